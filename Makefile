@@ -1,0 +1,38 @@
+# Build the product library (HIP, gfx950) and the CPU oracle (test infrastructure).
+HIPCC     ?= /opt/rocm/bin/hipcc
+ARCH      ?= gfx950
+PKG       := neural_polar_decoder_amd
+CSRC      := $(wildcard $(PKG)/csrc/*.hip)
+CHDR      := $(wildcard $(PKG)/csrc/*.hpp) include/npd.h
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -I$(PKG)/csrc \
+             -munsafe-fp-atomics
+LIB       := $(PKG)/libnpd.so
+OBJDIR    := build/obj
+OBJS      := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/%.o,$(CSRC))
+
+ORACLE    := oracle/liboracle.so
+
+all: $(LIB) $(ORACLE)
+
+lib: $(LIB)
+oracle: $(ORACLE)
+
+$(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(CHDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,--no-undefined
+
+# Oracle: plain C, no fast-math, no FMA contraction (exact restatement of the reference's fp32 ops).
+$(ORACLE): oracle/npd_oracle.c
+	gcc -O2 -std=c11 -fPIC -shared -fopenmp -ffp-contract=off -o $@ $< -lm
+
+asm: $(CSRC)
+	@mkdir -p build/asm
+	for f in $(CSRC); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/asm/$$(basename $$f .hip).s $$f; done
+
+clean:
+	rm -rf build $(LIB) $(ORACLE)
+
+.PHONY: all lib oracle clean asm

@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by IMPORTING the reference (never copying it).
+
+Run in the build container only (``/root/reference`` does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+Every fixture is data: inputs and the reference's outputs for them.  Reference functions called:
+  PolarCode.__init__ / encode_plotkin / channel / sc_decode_new       polar.py:66-148, 201-207, 465-484
+  PAC.__init__ / pac_encode / pac_sc_decode                           pac_code.py:97-224, 534-573
+  rnn_all.get_code                                                    rnn_all.py:1015-1196
+  RNN_Model / RNN_decoder.decode (test branch, y_input, onehot)       rnn_all.py:294-561
+  convNet.forward                                                     models.py:691-767
+  errors_ber / errors_bler                                            utils.py:17-51
+models.py imports IPython (absent here, not a reference requirement): a stub module is installed.
+"""
+import argparse
+import os
+import sys
+import types
+
+os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def _import_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit("reference not present: fixtures can only be generated in the build container")
+    sys.path.insert(0, REF)
+    ip = types.ModuleType("IPython")
+    ip.display = None
+    ip.get_ipython = lambda: None
+    sys.modules.setdefault("IPython", ip)
+    import polar, pac_code, utils, rnn_all, models  # noqa: E401
+    return polar, pac_code, utils, rnn_all, models
+
+
+polar_m, pac_m, utils_m, rnn_m, models_m = _import_reference()
+
+
+def ns(**kw):
+    d = dict(hard_decision=False, target_K=None, random_seed=42, loss_only=None, K=None, N=None)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def save(name, **arrs):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **arrs)
+    print("wrote", path, sum(np.asarray(v).nbytes for v in arrs.values()), "bytes raw")
+
+
+SNRS = np.array([0.0, 1.0, 2.0, 3.0, 4.0])
+
+
+# ------------------------------------------------------------------------------------------- codes
+def gen_codes():
+    out = {}
+    # get_code reads the module-global `args` of rnn_all (rnn_all.py:1015-1196)
+    for prof, N, K, tK in [("polar", 32, 16, 16), ("polar", 64, 32, 32), ("polar", 128, 64, 64),
+                           ("polar", 256, 128, 128), ("polar", 16, 8, 8), ("polar", 8, 4, 4), ("polar", 4, 2, 2),
+                           ("polar", 64, 22, 22), ("rev_polar", 64, 8, 22), ("rev_polar", 64, 22, 22),
+                           ("sorted", 64, 10, 22), ("sorted_last", 64, 10, 22), ("random", 64, 12, 22),
+                           ("RM", 64, 22, 22), ("RM", 32, 16, 16), ("rev_RM", 64, 10, 22)]:
+        rnn_m.args = ns(target_K=tK, K=K, N=N, random_seed=42)
+        code = rnn_m.get_code("Polar", prof, N, K)
+        out[f"polar_{prof}_{N}_{K}_{tK}"] = np.asarray(code.info_positions, np.int64)
+    for N, K in [(128, 64), (64, 22), (32, 16), (16, 11)]:
+        pac = pac_m.PAC(ns(target_K=K), N, K, 91)
+        out[f"pac_RM_{N}_{K}"] = np.asarray(pac.B, np.int64)
+    save("codes.npz", **out)
+
+
+# ----------------------------------------------------------------------------------------- encode
+def polar_code(N, K):
+    rnn_m.args = ns(target_K=K, K=K, N=N)
+    return rnn_m.get_code("Polar", "polar", N, K)
+
+
+def gen_encode():
+    g = torch.Generator().manual_seed(11)
+    out = {}
+    for N, K in [(32, 16), (64, 32), (128, 64), (256, 128), (8, 4)]:
+        code = polar_code(N, K)
+        msg = 1.0 - 2.0 * torch.randint(0, 2, (64, K), generator=g).float()
+        x = code.encode_plotkin(msg)
+        out[f"msg_{N}_{K}"] = msg.numpy()
+        out[f"x_{N}_{K}"] = x.numpy()
+        out[f"info_{N}_{K}"] = np.asarray(code.info_positions, np.int64)
+    # general float messages (not +-1): stage-order products
+    code = polar_code(16, 8)
+    msg = torch.randn(32, 8, generator=g)
+    out["msgf_16_8"] = msg.numpy()
+    out["xf_16_8"] = code.encode_plotkin(msg).numpy()
+    out["info_16_8"] = np.asarray(code.info_positions, np.int64)
+    for N, K in [(128, 64), (64, 22), (32, 16)]:
+        pac = pac_m.PAC(ns(target_K=K), N, K, 91)
+        msg = 1.0 - 2.0 * torch.randint(0, 2, (64, K), generator=g).float()
+        x = pac.pac_encode(msg, scheme="RM")
+        out[f"pmsg_{N}_{K}"] = msg.numpy()
+        out[f"px_{N}_{K}"] = x.numpy()
+        out[f"pinfo_{N}_{K}"] = np.asarray(pac.B, np.int64)
+    save("encode.npz", **out)
+
+
+# ------------------------------------------------------------------------------------------- SC
+def crafted_rows(N, rng):
+    rows = []
+    rows.append(np.zeros(N, np.float32))                     # every LLR exactly 0 -> sign(0) = 0 paths
+    r = rng.standard_normal(N).astype(np.float32)
+    r[rng.random(N) < 0.3] = 0.0                             # sparse exact zeros
+    rows.append(r)
+    r = (1.0 - 2.0 * (rng.random(N) < 0.5)).astype(np.float32) * 300.0  # |LLR| >> infty: frozen leaf < 0
+    rows.append(r)
+    r = rng.standard_normal(N).astype(np.float32) * 40.0
+    rows.append(r)
+    r = np.full(N, -1.0, np.float32)
+    rows.append(r)
+    return np.stack(rows)
+
+
+def gen_sc():
+    rng = np.random.default_rng(5)
+    for N, K, per in [(32, 16, 256), (64, 32, 256), (128, 64, 96), (256, 128, 48), (16, 8, 64), (64, 22, 128)]:
+        code = polar_code(N, K)
+        torch.manual_seed(1000 + N + K)
+        ys, snrs, leafs, hats, msgs = [], [], [], [], []
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (per, K)).float()
+            x = code.encode_plotkin(msg)
+            y = code.channel(x, float(snr))
+            leaf, hat = code.sc_decode_new(y, float(snr))
+            ys.append(y.numpy()); snrs.append(np.full(per, snr)); leafs.append(leaf.numpy()); hats.append(hat.numpy())
+            msgs.append(msg.numpy())
+        # crafted rows at 2 dB and 4 dB
+        for snr in (2.0, 4.0):
+            y = torch.from_numpy(crafted_rows(N, rng))
+            leaf, hat = code.sc_decode_new(y, snr)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); leafs.append(leaf.numpy())
+            hats.append(hat.numpy()); msgs.append(np.ones((y.shape[0], K), np.float32))
+        # genie (use_gt) path on a few rows
+        y = torch.from_numpy(np.concatenate(ys[:1])[:32])
+        gt = torch.from_numpy((1.0 - 2.0 * (rng.random((32, N)) < 0.5)).astype(np.float32))
+        gleaf, ghat = code.sc_decode_new(y, 1.0, use_gt=gt)
+        save(f"sc_polar_{N}_{K}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), leaf=np.concatenate(leafs),
+             msg_hat=np.concatenate(hats), msg=np.concatenate(msgs), info=np.asarray(code.info_positions, np.int64),
+             gt_y=y.numpy(), gt=gt.numpy(), gt_snr=np.float64(1.0), gt_leaf=gleaf.numpy(), gt_msg_hat=ghat.numpy())
+
+
+def gen_pac():
+    rng = np.random.default_rng(6)
+    for N, K, per in [(128, 64, 64), (64, 22, 96), (32, 16, 128)]:
+        pac = pac_m.PAC(ns(target_K=K), N, K, 91)
+        torch.manual_seed(77 + N)
+        ys, snrs, leafs, hats, uhs, msgs = [], [], [], [], [], []
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (per, K)).float()
+            x = pac.pac_encode(msg, scheme="RM")
+            y = pac.channel(x, float(snr))
+            leaf, hat, uh = pac.pac_sc_decode(y, float(snr))
+            ys.append(y.numpy()); snrs.append(np.full(per, snr)); leafs.append(leaf.numpy())
+            hats.append(hat.numpy()); uhs.append(uh.numpy()); msgs.append(msg.numpy())
+        for snr in (2.0, 4.0):
+            y = torch.from_numpy(crafted_rows(N, rng))
+            leaf, hat, uh = pac.pac_sc_decode(y, snr)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); leafs.append(leaf.numpy())
+            hats.append(hat.numpy()); uhs.append(uh.numpy()); msgs.append(np.ones((y.shape[0], K), np.float32))
+        y = torch.from_numpy(ys[1][:16])
+        gt = torch.from_numpy((1.0 - 2.0 * (rng.random((16, N)) < 0.5)).astype(np.float32))
+        gleaf, ghat, guh = pac.pac_sc_decode(y, 1.0, use_gt_codeword=gt)
+        save(f"sc_pac_{N}_{K}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), leaf=np.concatenate(leafs),
+             msg_hat=np.concatenate(hats), u_hat=np.concatenate(uhs), msg=np.concatenate(msgs),
+             info=np.asarray(pac.B, np.int64), gt_y=y.numpy(), gt=gt.numpy(), gt_snr=np.float64(1.0),
+             gt_leaf=gleaf.numpy(), gt_msg_hat=ghat.numpy(), gt_u_hat=guh.numpy())
+
+
+# ----------------------------------------------------------------------------------------- errors
+def gen_errors():
+    rng = np.random.default_rng(7)
+    ref = (1.0 - 2.0 * (rng.random((512, 32)) < 0.5)).astype(np.float32)
+    hat = ref.copy()
+    flip = rng.random(ref.shape) < 0.02
+    hat[flip] *= -1
+    hat[rng.random(ref.shape) < 0.01] = 0.0
+    t, h = torch.from_numpy(ref), torch.from_numpy(hat)
+    save("errors.npz", ref=ref, hat=hat, ber=np.float64(utils_m.errors_ber(t, h).item()),
+         bler=np.float64(utils_m.errors_bler(t, h)))
+
+
+# -------------------------------------------------------------------------------------------- GRU
+def gen_gru():
+    cases = [("gru_polar_64_32", "Polar", 64, 32, 64, True, False, 512),
+             ("gru_pac_128_64", "PAC", 128, 64, 64, True, False, 128),
+             ("gru_polar_16_8_noonehot_rev", "Polar", 16, 8, 16, False, True, 256)]
+    for name, ctype, N, K, F, onehot, rev, B in cases:
+        torch.manual_seed(2024 + N)
+        if ctype == "Polar":
+            code = polar_code(N, K)
+            info = np.asarray(code.info_positions, np.int64)
+        else:
+            code = pac_m.PAC(ns(target_K=K), N, K, 91)
+            info = np.asarray(code.B, np.int64)
+        net = rnn_m.RNN_Model("GRU", N + 1 + int(onehot), F, 1, 2, N, 0, 0, "selu", 0.0, False,
+                              out_linear_depth=1)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_input", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits = [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            x = code.encode_plotkin(msg) if ctype == "Polar" else code.pac_encode(msg, scheme="RM")
+            y = code.channel(x, float(snr))
+            rec.clear()
+            d = dec.decode(net, False, y)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, onehot=int(onehot), rev=int(rev),
+             **{"w." + k: v for k, v in sd.items()})
+
+
+# ------------------------------------------------------------------------------------------- conv
+def conv_weights_from_seed(embed, N, seed):
+    """Documented deterministic generator (mirrored in tests/conftest.py): PCG64(seed); each parameter,
+    in state_dict order, ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (PyTorch's default bound); LayerNorm
+    weight = 1 + 0.1*U(-1,1), bias = 0.1*U(-1,1)."""
+    cfg = argparse.Namespace(embed_dim=embed, max_len=N, N=N, dont_use_bias=False, dropout=0.0)
+    net = models_m.convNet(cfg)
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for k, v in net.state_dict().items():
+        shape = tuple(v.shape)
+        if k.startswith("layer_norm"):
+            a = rng.uniform(-1, 1, size=shape)
+            arr = (1.0 + 0.1 * a) if k.endswith("weight") else 0.1 * a
+        else:
+            wname = k.rsplit(".", 1)[0] + ".weight"
+            ws = tuple(net.state_dict()[wname].shape)
+            fan_in = int(np.prod(ws[1:]))
+            bnd = 1.0 / np.sqrt(fan_in)
+            arr = rng.uniform(-bnd, bnd, size=shape)
+        sd[k] = torch.from_numpy(arr.astype(np.float32))
+    net.load_state_dict(sd)
+    net.eval()
+    return net, {k: v.numpy() for k, v in sd.items()}
+
+
+def gen_conv():
+    for name, embed, N, K, B, store_w in [("conv_small_64", 16, 64, 32, 64, True),
+                                          ("conv_c5_256", 128, 256, 128, 16, False)]:
+        net, sd = conv_weights_from_seed(embed, N, seed=4242 + embed)
+        code = polar_code(N, K)
+        torch.manual_seed(99)
+        msg = 1.0 - 2.0 * torch.randint(0, 2, (B, K)).float()
+        y = code.channel(code.encode_plotkin(msg), 1.0)
+        with torch.no_grad():
+            out = net.forward(y, None, None, "cpu")
+        logits = out[3].view(B, N).numpy()
+        dec = out[1].view(B, N).numpy()
+        extra = {"w." + k: v for k, v in sd.items()} if store_w else {}
+        save(f"{name}.npz", y=y.numpy(), logits=logits, decoded=dec, embed=embed, N=N, seed=4242 + embed, **extra)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["codes", "encode", "sc", "pac", "errors", "gru", "conv"]
+    for w in which:
+        globals()["gen_" + w]()
