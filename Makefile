@@ -17,9 +17,12 @@ all: $(LIB) $(ORACLE)
 lib: $(LIB)
 oracle: $(ORACLE)
 
+# per-file extras: the SC kernel never sees NaN (finite LLRs), so fmin needs no canonicalisation
+EXTRA_npd_sc := -fno-honor-nans
+
 $(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(CHDR)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(EXTRA_$*) -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,--no-undefined
@@ -30,7 +33,7 @@ $(ORACLE): oracle/npd_oracle.c
 
 asm: $(CSRC)
 	@mkdir -p build/asm
-	for f in $(CSRC); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/asm/$$(basename $$f .hip).s $$f; done
+	for f in $(CSRC); do b=$$(basename $$f .hip); $(HIPCC) $(HIPFLAGS) $$( [ $$b = npd_sc ] && echo -fno-honor-nans ) --cuda-device-only -S -o build/asm/$$b.s $$f; done
 
 clean:
 	rm -rf build $(LIB) $(ORACLE)

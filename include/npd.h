@@ -1,0 +1,156 @@
+/*
+ * npd.h -- C ABI of libnpd.so, the MI355X-native batch Polar/PAC decoding hot path.
+ *
+ * The reference (hebbarashwin/neural_polar_decoder) is pure Python/PyTorch with no FFI; its
+ * "operator API" for this path is the Python method surface of PolarCode / PAC / RNN_decoder /
+ * convNet.  Each entry point below replaces one of those methods (cited per function); the Python
+ * mirror in neural_polar_decoder_amd/ binds them with ctypes.
+ *
+ * Conventions
+ *   - All tensor pointers are DEVICE pointers owned by the caller (e.g. torch tensors' data_ptr()),
+ *     row-major fp32 unless stated: y/x (B,N), msg/msg_hat (B,K), exactly the reference's layouts.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  Every call is
+ *     stream-ordered and asynchronous; none allocates or synchronises, so calls can be captured
+ *     into a hipGraph.
+ *   - Handles (npd_code, npd_gru, npd_conv) are immutable after creation: concurrent use from
+ *     several host threads on distinct streams is safe.  A handle is bound to the device that was
+ *     current when it was created.
+ *   - Return value: 0 = success; > 0 = hipError_t passthrough; < 0 = argument error (NPD_E*).
+ *     npd_last_error() returns a thread-local description of the last failure.  Nothing aborts.
+ *   - Random numbers: Philox4x32-10, counter = (block, stream, codeword index), key = seed, so
+ *     results are independent of how codewords are sharded over launches or GPUs.
+ */
+#ifndef NPD_H_
+#define NPD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NPD_ABI_VERSION 1
+
+#define NPD_OK 0
+#define NPD_EINVAL (-1)   /* bad argument (null pointer, size, unsupported N/K) */
+#define NPD_ENOTSUP (-2)  /* configuration not compiled in */
+#define NPD_ENOMEM (-3)   /* host allocation failed */
+
+typedef struct npd_code npd_code; /* a Polar or PAC code: N, K, info set, frozen prior, PAC taps */
+typedef struct npd_gru npd_gru;   /* a CRISP GRU decoder's weights, repacked for the kernel */
+typedef struct npd_conv npd_conv; /* a convNet decoder's weights, repacked for the kernel */
+
+int npd_abi_version(void);
+const char* npd_last_error(void);
+/* number of visible HIP devices (0 when none); never fails */
+int npd_device_count(void);
+
+/* ---------------------------------------------------------------------------------- codes */
+/*
+ * Create a code.  Replaces PolarCode.__init__ (polar.py:66-117) and PAC.__init__/rate_profiler
+ * (pac_code.py:97-174): the caller passes the sorted information set it computed (rate profiles
+ * are host logic).  pac_g == 0 -> Polar code; otherwise the PAC convolution polynomial (91 in the
+ * reference; its top bit must be set).  infty = the Polar frozen-leaf prior (polar.py:66, default
+ * 1000), ignored for PAC (pac_sc_decode applies no prior).  4 <= N <= 256, N a power of two.
+ */
+int npd_code_create(int N, int K, const int32_t* info_sorted, int pac_g, float infty, npd_code** out);
+int npd_code_destroy(npd_code* code);
+
+/* ---------------------------------------------------------------------------------- encode */
+/*
+ * x = encode(msg).  Polar: PolarCode.encode_plotkin (polar.py:128-148) -- u = ones, u[info] = msg,
+ * butterfly left *= right for d = 0..n-1 (bit-exact for any fp32 input, same product order).
+ * PAC: PAC.pac_encode (pac_code.py:220-224) -- rate profile, conv pre-transform, rate-1 Plotkin.
+ */
+int npd_encode(const npd_code* code, const float* msg, float* x, int64_t B, void* stream);
+
+/* ---------------------------------------------------------------------------------- channel */
+/*
+ * y = x + fl32(sigma) * n, n ~ N(0,1) from Philox stream (seed, snr_index), codeword index
+ * cw_offset + b.  Replaces PolarCode.channel / PAC.channel (polar.py:201-207, pac_code.py:226-231).
+ * N % 4 == 0.
+ */
+int npd_awgn(const float* x, float* y, int64_t B, int N, float sigma, uint64_t seed, uint32_t snr_index,
+             uint64_t cw_offset, void* stream);
+
+/*
+ * Fused Monte-Carlo data generation for codewords cw_offset .. cw_offset+B-1: msg bits from Philox
+ * (seed), encode (Polar or PAC), AWGN at (sigma, snr_index).  Any of msg/x may be NULL; y required.
+ * Equivalent to msg = 1-2*bits; x = encode(msg); y = channel(x, snr) in the reference eval loops
+ * (run_models.py:318-323, rnn_all.py:842-847).
+ */
+int npd_mc_generate(const npd_code* code, float* msg, float* x, float* y, int64_t B, float sigma, uint64_t seed,
+                    uint32_t snr_index, uint64_t cw_offset, void* stream);
+
+/* ---------------------------------------------------------------------------------- SC decode */
+/*
+ * Successive-cancellation min-sum decoding, one codeword per lane.
+ * Polar: PolarCode.sc_decode_new (polar.py:465-484): LLR = llr_scale * y with
+ *   llr_scale = fl32(2/sigma^2); f = sign(a)sign(b)min(|a|,|b|) (utils.py:272-275); g = u*a + b;
+ *   leaf = L + infty on frozen positions; u = sign(leaf).  Outputs: leaf_llr (B,N) [optional],
+ *   msg_hat = u[:, info] (B,K) [optional].  u_hat must be NULL.
+ * PAC: PAC.pac_sc_decode (pac_code.py:534-573): same tree, no prior, conv-state leaf rule.
+ *   Outputs: leaf_llr (B,N), msg_hat = v_hat[:, info] (B,K), u_hat (B,N); each optional.
+ * gt (B,N) optional genie (use_gt polar.py:480 / use_gt_codeword pac_code.py:548-555), else NULL.
+ * Decisions and leaf LLRs are bit-exact with the reference (fp32, same operation order).
+ */
+int npd_sc_decode(const npd_code* code, const float* y, float llr_scale, float* leaf_llr, float* msg_hat,
+                  float* u_hat, const float* gt, int64_t B, void* stream);
+
+/*
+ * Monte-Carlo SC decode with fused error counting: decodes y (B,N) of codewords
+ * cw_offset .. cw_offset+B-1 whose messages are the Philox message stream of `seed` (as written
+ * by npd_mc_generate), writes msg_hat (B,K) if non-NULL, and adds {bit errors, block errors} to
+ * counters[0..1] (device uint64, not reset).  Error semantics of errors_ber/errors_bler
+ * (utils.py:17-51): a decision of 0 counts as an error.
+ */
+int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_scale, float* msg_hat, uint64_t seed,
+                     uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream);
+
+/* ---------------------------------------------------------------------------------- counters */
+/*
+ * counters[0] += #(round(ref) != round(hat)), counters[1] += #rows with any such element, over
+ * (B,K) fp32 arrays.  Replaces errors_ber / errors_bler's counting (utils.py:17-51) with device
+ * uint64 counters (no host sync per batch).
+ */
+int npd_count_errors(const float* ref, const float* hat, int64_t B, int K, unsigned long long* counters,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------------- CRISP GRU */
+/*
+ * Create a GRU decoder from an RNN_Model state dict (rnn_all.py:294-398): nn.GRU(input_size, F,
+ * layers, batch_first) + Linear(F, 1), decoding_type y_input without the y-MLP.
+ * weights: host fp32, packed per layer l = 0..layers-1 as
+ *   weight_ih_l (3F, Din_l) | weight_hh_l (3F, F) | bias_ih_l (3F) | bias_hh_l (3F),
+ * then linear.weight (F) | linear.bias (1); Din_0 = N + 2 (onehot) or N + 1, Din_l = F for l > 0.
+ * precision: 0 = fp32 (default, exact fp32 FMA chains), 1 = bf16x3 split, 2 = bf16.
+ */
+int npd_gru_create(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
+                   npd_gru** out);
+int npd_gru_destroy(npd_gru* gru);
+/*
+ * RNN_decoder.decode(net, False, y, gt) test branch (rnn_all.py:532-547): decoded (B,N) fp32, with
+ * decoded[:, i] = sign(out_i) for i in the info set (is_info: N bytes, host) and 1 (or gt) else.
+ * reverse: RNN_decoder reverse_order (rnn_all.py:414-416).  logits (B,N) optional: raw output at
+ * every step.
+ */
+int npd_gru_decode(const npd_gru* gru, const float* y, const uint8_t* is_info, int reverse, const float* gt,
+                   float* decoded, float* logits, int64_t B, void* stream);
+
+/* ---------------------------------------------------------------------------------- conv model */
+/*
+ * convNet (models.py:691-772) forward/decode.  weights: host fp32 in state_dict order
+ * (layers1.0.weight, layers1.0.bias, ..., layersFin.4.bias, layer_norm.weight, layer_norm.bias).
+ * embed = config.embed_dim (even), N = config.N = config.max_len.
+ */
+int npd_conv_create(int N, int embed, const float* weights, int64_t n_weights, int precision, npd_conv** out);
+int npd_conv_destroy(npd_conv* conv);
+/* logits (B,N) and/or decoded = sign(logits) (B,N); workspace sized by npd_conv_workspace_bytes */
+int64_t npd_conv_workspace_bytes(const npd_conv* conv, int64_t B);
+int npd_conv_forward(const npd_conv* conv, const float* y, float* logits, float* decoded, void* workspace,
+                     int64_t B, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NPD_H_ */

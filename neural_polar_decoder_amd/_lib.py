@@ -1,0 +1,96 @@
+"""ctypes binding of libnpd.so (include/npd.h).
+
+The product path has exactly one implementation: the HIP kernels in libnpd.so.  If the library is
+missing or no GPU is visible, every compute call raises :class:`NpdError` -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NPD_LIB", os.path.join(_HERE, "libnpd.so"))
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_float = ctypes.c_float
+
+# (name, restype, argtypes) -- must match include/npd.h exactly (tests check every symbol)
+SIGNATURES = [
+    ("npd_abi_version", c_int, []),
+    ("npd_last_error", ctypes.c_char_p, []),
+    ("npd_device_count", c_int, []),
+    ("npd_code_create", c_int, [c_int, c_int, c_void_p, c_int, c_float, ctypes.POINTER(c_void_p)]),
+    ("npd_code_destroy", c_int, [c_void_p]),
+    ("npd_encode", c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    ("npd_awgn", c_int, [c_void_p, c_void_p, c_i64, c_int, c_float, c_u64, c_u32, c_u64, c_void_p]),
+    ("npd_mc_generate", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_float, c_u64, c_u32, c_u64,
+                                c_void_p]),
+    ("npd_sc_decode", c_int, [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    ("npd_sc_decode_mc", c_int, [c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_i64, c_void_p, c_void_p]),
+    ("npd_count_errors", c_int, [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p]),
+    ("npd_gru_create", c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
+    ("npd_gru_destroy", c_int, [c_void_p]),
+    ("npd_gru_decode", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    ("npd_conv_create", c_int, [c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
+    ("npd_conv_destroy", c_int, [c_void_p]),
+    ("npd_conv_workspace_bytes", c_i64, [c_void_p, c_i64]),
+    ("npd_conv_forward", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+]
+
+
+class NpdError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libnpd.so (raises NpdError if it is missing -- build it with `make lib`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NpdError(f"libnpd.so not found at {LIB_PATH}; build it with `make` or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = load().npd_last_error()
+        raise NpdError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def require_gpu(t: torch.Tensor, name: str):
+    """The product path runs only on the GPU: fail loudly for host tensors."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise NpdError(f"{name} must be a device (HIP) tensor: libnpd has no CPU path")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def f32c(t: torch.Tensor) -> torch.Tensor:
+    """contiguous fp32 view/copy on the same device"""
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()

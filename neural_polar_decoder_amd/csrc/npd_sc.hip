@@ -1,0 +1,548 @@
+// npd_sc.hip -- successive-cancellation min-sum decoding (Polar and PAC) for gfx950.
+//
+// Replaces PolarCode.sc_decode_new (polar.py:361-484) and PAC.pac_sc_decode (pac_code.py:233-345,
+// 534-573).  The reference re-walks the code tree for every leaf with torch.cat/clone on (B, n+1, N)
+// arrays; here one lane owns one codeword and runs the whole SC schedule fully unrolled at compile
+// time, so every LLR and partial sum lives at a fixed register (or LDS row) address.
+//
+// Data path per wave (64 codewords = one "tile"):
+//   HBM y tile (64 x N fp32, contiguous) --global_load_lds_dwordx4, 1 KiB per instruction,
+//   XOR-swizzled chunk order--> LDS staging --ds_read_b128, conflict-free--> VGPRs (LLR levels with
+//   node size <= R) / LDS rows (levels with node size > R) --> decisions written per leaf into an
+//   LDS row (stride N+1 floats, conflict-free) --> coalesced dword stores of msg_hat / leaf / u_hat.
+//
+// Arithmetic is exactly the reference's fp32 sequence:
+//   L = fl32(llr_scale * y);  f(a,b) = min(|a|,|b|)*sign(a)*sign(b) (utils.py:272-275) -- computed as
+//   min(|a|,|b|) with the xor of the sign bits (identical value, +-0 aside);  g = u*a + b (u in
+//   {-1,0,1}, so the product is exact and fma == mul+add);  leaf = L + prior (polar.py:438, 446);
+//   u = sign(leaf) (polar.py:479).  Partial sums of finished R-blocks are kept as sign/zero bit masks.
+#include "npd_common.hpp"
+
+namespace npd {
+namespace sc {
+
+enum Flags : uint32_t {
+    kLeaf = 1u << 0,   // write leaf LLRs (B,N)
+    kMsg = 1u << 1,    // write msg_hat (B,K)
+    kUhat = 1u << 2,   // write u_hat (B,N) (PAC)
+    kGt = 1u << 3,     // genie decisions from gt (B,N)
+    kCount = 1u << 4,  // count errors against the Philox message stream
+};
+
+struct Args {
+    const float* y;
+    float* leaf;
+    float* msg;
+    float* uhat;
+    const float* gt;
+    unsigned long long* counters;
+    uint64_t seed;
+    uint64_t cw_offset;
+    int64_t B;
+    int64_t ntiles;
+    float scale;
+    uint32_t flags;
+    // byte offsets inside the dynamic LDS block of the (single-wave) workgroup
+    uint32_t off_stage, off_u, off_v, off_leaf, off_gt, off_info, off_lvl;
+};
+
+// ------------------------------------------------------------------------------ small helpers
+__device__ __forceinline__ float f_minsum(float a, float b) {
+    const float m = __builtin_fminf(__builtin_fabsf(a), __builtin_fabsf(b));
+    return bitsf(fbits(m) | ((fbits(a) ^ fbits(b)) & 0x80000000u));
+}
+
+// sign(x) in {-1, 0, +1} (torch.sign): copy the sign bit onto 1.0, 0 for +-0
+__device__ __forceinline__ float sgn_bits(float x) {
+    const float s = bitsf((fbits(x) & 0x80000000u) | 0x3f800000u);
+    return (x == 0.0f) ? 0.0f : s;
+}
+
+// g with the left partial sum given as sign/zero bits of one position
+__device__ __forceinline__ float g_bits(uint32_t sw, uint32_t zw, int bit, float a, float b) {
+    const float s = bitsf(fbits(a) ^ ((sw << (31 - bit)) & 0x80000000u)) + b;
+    return ((zw >> bit) & 1u) ? b : s;
+}
+
+template <int C>
+__device__ __forceinline__ int swz(int r) {
+    if constexpr (C >= 16) return r & 15;
+    else return (r / (16 / C)) % C;
+}
+
+template <int N>
+struct Geo {
+    static constexpr int C = N / 4;  // 16-B chunks per row
+    static constexpr int NP = N + 1; // padded row stride (floats) for per-lane rows
+};
+
+// ------------------------------------------------------------------------------ per-lane context
+template <int N, int R, bool PAC, bool FULL>
+struct Ctx {
+    static constexpr int NW = (N + 31) / 32;
+    float lv[2 * R];      // register LLR levels: level d (2^d <= R) at lv[2^d .. 2^(d+1))
+    float beta[R];        // partial sums of the current R-block
+    uint32_t S[NW], Z[NW];  // sign / zero bits of partial sums of completed R-blocks (N > R only)
+    uint32_t st;          // PAC conv state (bit t = 1 iff state[t] == -1)
+    // LDS row bases (bytes) of this lane
+    char* lds;
+    uint32_t stage_row;   // staging chunk base for this lane's row (chunk index r*C)
+    int sw;               // this lane's swizzle
+    uint32_t u_row, v_row, leaf_row, gt_row;
+    uint32_t lvl_row[9];  // per-level LDS rows for upper levels (node size > R, < N)
+    float scale;
+    uint32_t flags;
+};
+
+template <int N>
+__device__ __forceinline__ float4 stage_chunk(char* lds, uint32_t off_stage, uint32_t row_chunk, int sw, int c) {
+    const uint32_t addr = off_stage + ((row_chunk + (uint32_t)(c ^ sw)) << 4);
+    return *reinterpret_cast<const float4*>(lds + addr);
+}
+
+__device__ __forceinline__ void lds_wr(char* lds, uint32_t byte, float v) { *reinterpret_cast<float*>(lds + byte) = v; }
+__device__ __forceinline__ float lds_rd(const char* lds, uint32_t byte) { return *reinterpret_cast<const float*>(lds + byte); }
+
+// ------------------------------------------------------------------------------ leaf
+template <int N, int R, bool PAC, bool FULL, int I>
+__device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a, float L) {
+    const bool frozen = (p.frozen[I >> 5] >> (I & 31)) & 1u;
+    float u;
+    if constexpr (!PAC) {
+        // polar.py:438/446: leaf = L + prior; prior = infty on frozen positions, 0 elsewhere
+        const float lf = L + (frozen ? p.infty : 0.0f);
+        if (FULL && (c.flags & kLeaf)) lds_wr(c.lds, c.leaf_row + 4 * I, lf);
+        if (FULL && (c.flags & kGt)) u = lds_rd(c.lds, c.gt_row + 4 * I);
+        else u = sgn_bits(lf);
+    } else {
+        if (FULL && (c.flags & kLeaf)) lds_wr(c.lds, c.leaf_row + 4 * I, L);
+        const float u0 = (__builtin_popcount(c.st & p.tapmask) & 1) ? -1.0f : 1.0f;  // conv(+1) (pac_code.py:188-193)
+        float v;
+        if (frozen) {  // pac_code.py:545-551
+            v = 1.0f;
+            if (FULL && (c.flags & kGt)) {
+                u = lds_rd(c.lds, c.gt_row + 4 * I);
+            } else {
+                u = u0;
+                c.st = (c.st << 1) & p.smask;
+            }
+        } else {  // pac_code.py:553-568
+            u = (FULL && (c.flags & kGt)) ? lds_rd(c.lds, c.gt_row + 4 * I) : sgn_bits(L);
+            if (u == u0) {
+                v = 1.0f;
+                c.st = (c.st << 1) & p.smask;
+            } else if (u == -u0) {
+                v = -1.0f;
+                c.st = ((c.st << 1) | 1u) & p.smask;
+            } else {
+                v = 0.0f;
+            }
+        }
+        lds_wr(c.lds, c.v_row + 4 * I, v);
+    }
+    lds_wr(c.lds, c.u_row + 4 * I, u);
+    c.beta[I % R] = u;
+}
+
+// ------------------------------------------------------------------------------ register levels
+// node at depth D (2^D <= R) covering absolute leaves [S0, S0 + 2^D); its LLRs at lv[2^D ..]
+template <int N, int R, bool PAC, bool FULL, int D, int S0>
+__device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a) {
+    if constexpr (D == 0) {
+        leaf<N, R, PAC, FULL, S0>(c, p, a, c.lv[1]);
+    } else {
+        constexpr int h = 1 << (D - 1);
+        constexpr int bs = S0 % R;  // local beta base
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
+        node_reg<N, R, PAC, FULL, D - 1, S0>(c, p, a);
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[bs + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+        node_reg<N, R, PAC, FULL, D - 1, S0 + h>(c, p, a);
+        if constexpr ((1 << D) < N) {  // the root's combined partial sums are never used
+#pragma unroll
+            for (int j = 0; j < h; ++j) c.beta[bs + j] = c.beta[bs + j] * c.beta[bs + h + j];
+        }
+    }
+}
+
+// pack the float partial sums of a finished R-block starting at absolute position S0 into bits
+template <int N, int R, bool PAC, bool FULL, int S0>
+__device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL>& c) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int pos = S0 + j;
+        const float b = c.beta[j];
+        const uint32_t sb = (b < 0.0f) ? 1u : 0u;
+        const uint32_t zb = (b == 0.0f) ? 1u : 0u;
+        if ((pos & 31) == 0) {
+            c.S[pos >> 5] = sb;
+            c.Z[pos >> 5] = zb;
+        } else {
+            c.S[pos >> 5] |= sb << (pos & 31);
+            c.Z[pos >> 5] |= zb << (pos & 31);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ upper levels
+// value j of the level-D LLR vector of the current node (D = n: staging input scaled; else LDS row)
+template <int N, int R, bool PAC, bool FULL, int D>
+__device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL>& c, const Args& a, int j) {
+    (void)a;
+    if constexpr ((1 << D) == N) {
+        // staging: element j of the row is in chunk j/4, sub j%4
+        const uint32_t addr = a.off_stage + ((c.stage_row + (uint32_t)((j >> 2) ^ c.sw)) << 4) + 4 * (j & 3);
+        return c.scale * lds_rd(c.lds, addr);
+    } else {
+        return lds_rd(c.lds, c.lvl_row[D] + 4 * j);
+    }
+}
+
+template <int N, int R, bool PAC, bool FULL, int D>
+__device__ __forceinline__ void up_put(Ctx<N, R, PAC, FULL>& c, int j, float v) {
+    if constexpr ((1 << D) == R) c.lv[R + j] = v;
+    else lds_wr(c.lds, c.lvl_row[D] + 4 * j, v);
+}
+
+template <int N, int R, bool PAC, bool FULL, int D, int S0>
+__device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a) {
+    if constexpr ((1 << D) == R) {
+        node_reg<N, R, PAC, FULL, D, S0>(c, p, a);
+        pack_block<N, R, PAC, FULL, S0>(c);
+    } else {
+        constexpr int h = 1 << (D - 1);
+        if constexpr ((1 << D) == N) {
+            // read the staging row chunk-wise (4 values of a and of b per pair of ds_read_b128)
+#pragma unroll
+            for (int q = 0; q < h / 4; ++q) {
+                const float4 A = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q);
+                const float4 Bv = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q + h / 4);
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 0, f_minsum(c.scale * A.x, c.scale * Bv.x));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 1, f_minsum(c.scale * A.y, c.scale * Bv.y));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 2, f_minsum(c.scale * A.z, c.scale * Bv.z));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 3, f_minsum(c.scale * A.w, c.scale * Bv.w));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < h; ++j)
+                up_put<N, R, PAC, FULL, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, D>(c, a, j), up_get<N, R, PAC, FULL, D>(c, a, j + h)));
+        }
+        node_up<N, R, PAC, FULL, D - 1, S0>(c, p, a);
+        if constexpr ((1 << D) == N) {
+#pragma unroll
+            for (int q = 0; q < h / 4; ++q) {
+                const float4 A = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q);
+                const float4 Bv = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q + h / 4);
+                const float av[4] = {A.x, A.y, A.z, A.w};
+                const float bv[4] = {Bv.x, Bv.y, Bv.z, Bv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = S0 + 4 * q + e;
+                    up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + e,
+                                             g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, c.scale * av[e], c.scale * bv[e]));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < h; ++j) {
+                const int pos = S0 + j;
+                up_put<N, R, PAC, FULL, D - 1>(c, j, g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, up_get<N, R, PAC, FULL, D>(c, a, j),
+                                                      up_get<N, R, PAC, FULL, D>(c, a, j + h)));
+            }
+        }
+        node_up<N, R, PAC, FULL, D - 1, S0 + h>(c, p, a);
+        if constexpr ((1 << D) < N) {
+            // combine bit partial sums: left *= right  (h >= 64: whole words)
+#pragma unroll
+            for (int w = 0; w < h / 32; ++w) {
+                c.S[(S0 >> 5) + w] ^= c.S[((S0 + h) >> 5) + w];
+                c.Z[(S0 >> 5) + w] |= c.Z[((S0 + h) >> 5) + w];
+            }
+        }
+    }
+}
+
+template <int N>
+constexpr int log2c() {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    return n;
+}
+
+// ------------------------------------------------------------------------------ output pass
+// store W floats per row for the tile's `rows` valid rows: value(r, col) = lds[base + r*stride + 4*map(col)]
+__device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint32_t stride_b, const int32_t* info_lds,
+                                           int W, float* out, int64_t tile_row0, int rows, int lane) {
+    if (out == nullptr || W == 0) return;
+    float* dst = out + tile_row0 * (int64_t)W;
+    const int total = rows * W;
+    int r = lane / W, col = lane % W;
+    const int dr = kWave / W, dc = kWave % W;
+    for (int e = lane; e < total; e += kWave) {
+        const int m = info_lds ? info_lds[col] : col;
+        dst[e] = lds_rd(lds, base + (uint32_t)r * stride_b + 4u * (uint32_t)m);
+        r += dr;
+        col += dc;
+        if (col >= W) {
+            col -= W;
+            ++r;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ kernel
+template <int N, int R, bool PAC, bool FULL>
+__global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int n = log2c<N>();
+    constexpr int C = Geo<N>::C;
+    constexpr int NP = Geo<N>::NP;
+    const int lane = threadIdx.x;
+
+    Ctx<N, R, PAC, FULL> c;
+    c.lds = lds;
+    c.scale = a.scale;
+    c.flags = a.flags;
+    c.sw = swz<C>(lane);
+    c.stage_row = (uint32_t)(lane * C);
+    c.u_row = a.off_u + (uint32_t)(lane * NP * 4);
+    c.v_row = a.off_v + (uint32_t)(lane * NP * 4);
+    c.leaf_row = a.off_leaf + (uint32_t)(lane * NP * 4);
+    c.gt_row = a.off_gt + (uint32_t)(lane * NP * 4);
+    {
+        uint32_t off = a.off_lvl;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            c.lvl_row[d] = 0;
+            if ((1 << d) > R && (1 << d) < N) {
+                c.lvl_row[d] = off + (uint32_t)(lane * ((1 << d) + 1) * 4);
+                off += (uint32_t)(kWave * ((1 << d) + 1) * 4);
+            }
+        }
+    }
+    int32_t* info_lds = reinterpret_cast<int32_t*>(lds + a.off_info);
+    for (int k = lane; k < p.K; k += kWave) info_lds[k] = p.info[k];
+
+    uint32_t err_bits = 0, err_blocks = 0;
+    const bool count = (a.flags & kCount) != 0;
+
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t row0 = t * kWave;
+        const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
+
+        // ---- stage the y tile: C x 1 KiB global_load_lds, swizzled source addresses
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const int pch = k * kWave + lane;
+            const int r = pch / C;
+            const int q = pch % C;
+            const int cc = q ^ swz<C>(r);
+            int64_t grow = row0 + r;
+            if (grow >= a.B) grow = a.B - 1;
+            const float* src = a.y + grow * N + cc * 4;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(lds + a.off_stage + k * 1024), 16, 0, 0);
+        }
+        if (FULL && (a.flags & kGt)) {
+            for (int e = lane; e < kWave * N; e += kWave) {
+                const int r = e / N, col = e % N;
+                int64_t grow = row0 + r;
+                if (grow >= a.B) grow = a.B - 1;
+                lds_wr(lds, a.off_gt + (uint32_t)((r * NP + col) * 4), a.gt[grow * N + col]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+        c.st = 0;
+        if constexpr (R == N) {
+            // whole row into registers
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                const float4 v = stage_chunk<N>(lds, a.off_stage, c.stage_row, c.sw, q);
+                c.lv[N + 4 * q + 0] = c.scale * v.x;
+                c.lv[N + 4 * q + 1] = c.scale * v.y;
+                c.lv[N + 4 * q + 2] = c.scale * v.z;
+                c.lv[N + 4 * q + 3] = c.scale * v.w;
+            }
+            node_reg<N, R, PAC, FULL, n, 0>(c, p, a);
+        } else {
+            node_up<N, R, PAC, FULL, n, 0>(c, p, a);
+        }
+
+        // ---- error counting against the Philox message stream (utils.py:17-51 semantics)
+        if (count) {
+            const uint64_t cw = a.cw_offset + (uint64_t)(row0 + lane);
+            const uint32_t dec_row = PAC ? c.v_row : c.u_row;
+            uint32_t e = 0;
+#pragma unroll
+            for (int blk = 0; blk < (N + 127) / 128; ++blk) {
+                if (blk * 128 < p.K) {
+                    const u32x4 o = philox_block(a.seed, kStreamMsg, cw, (uint32_t)blk);
+                    const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const int k0 = blk * 128 + w * 32;
+                        const int kn = (p.K - k0) < 32 ? (p.K - k0) : 32;
+                        uint32_t bits = w4[w];
+                        for (int j = 0; j < kn; ++j) {
+                            const int pos = info_lds[k0 + j];  // wave-uniform LDS address: broadcast
+                            const float u = lds_rd(lds, dec_row + 4u * (uint32_t)pos);
+                            const float m = (bits & 1u) ? -1.0f : 1.0f;
+                            bits >>= 1;
+                            e += (u != m) ? 1u : 0u;
+                        }
+                    }
+                }
+            }
+            if (lane < rows) {
+                err_bits += e;
+                err_blocks += (e > 0) ? 1u : 0u;
+            }
+        }
+
+        // ---- coalesced output stores
+        if (a.flags & kMsg)
+            store_rows(lds, PAC ? a.off_v : a.off_u, NP * 4, info_lds, p.K, a.msg, row0, rows, lane);
+        if (FULL && (a.flags & kLeaf)) store_rows(lds, a.off_leaf, NP * 4, nullptr, N, a.leaf, row0, rows, lane);
+        if (FULL && (a.flags & kUhat)) store_rows(lds, a.off_u, NP * 4, nullptr, N, a.uhat, row0, rows, lane);
+    }
+
+    if (count) {
+        const uint32_t eb = wave_sum_u32(err_bits);
+        const uint32_t bl = wave_sum_u32(err_blocks);
+        if (lane == 0) {
+            atomicAdd(a.counters + 0, (unsigned long long)eb);
+            atomicAdd(a.counters + 1, (unsigned long long)bl);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ host side
+struct Layout {
+    uint32_t off_stage, off_u, off_v, off_leaf, off_gt, off_info, off_lvl, total;
+};
+
+static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+template <int N, int R>
+static Layout make_layout(bool pac, uint32_t flags) {
+    Layout L{};
+    const uint32_t stage = (uint32_t)(kWave * N * 4);
+    const uint32_t row = (uint32_t)(kWave * (N + 1) * 4);
+    uint32_t off = 0;
+    L.off_stage = 0;
+    if (R == N) {
+        // the staged tile is fully read into registers before the first decision is written:
+        // the decision rows alias the staging buffer
+        L.off_u = 0;
+        off = align16(stage > row ? stage : row);
+    } else {
+        off = align16(stage);
+        L.off_u = off;
+        off = align16(off + row);
+    }
+    L.off_v = pac ? off : 0;
+    if (pac) off = align16(off + row);
+    L.off_leaf = (flags & kLeaf) ? off : 0;
+    if (flags & kLeaf) off = align16(off + row);
+    L.off_gt = (flags & kGt) ? off : 0;
+    if (flags & kGt) off = align16(off + row);
+    L.off_lvl = off;
+    for (int d = 0; d < 9; ++d)
+        if ((1 << d) > R && (1 << d) < N) off += (uint32_t)(kWave * ((1 << d) + 1) * 4);
+    off = align16(off);
+    L.off_info = off;
+    off = align16(off + (uint32_t)(N * 4));
+    L.total = off;
+    return L;
+}
+
+template <int N, int R, bool PAC, bool FULL>
+static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
+    const Layout L = make_layout<N, R>(PAC, a.flags);
+    a.off_stage = L.off_stage;
+    a.off_u = L.off_u;
+    a.off_v = L.off_v;
+    a.off_leaf = L.off_leaf;
+    a.off_gt = L.off_gt;
+    a.off_info = L.off_info;
+    a.off_lvl = L.off_lvl;
+    a.ntiles = (a.B + kWave - 1) / kWave;
+    auto kern = sc_decode_kernel<N, R, PAC, FULL>;
+    static bool attr_set[2] = {false, false};  // per instantiation; benign race (idempotent)
+    if (!attr_set[0] && L.total > 65536) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr_set[0] = true;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, L.total) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), L.total, stream, p, a);
+    return launch_check("sc_decode_kernel launch");
+}
+
+template <bool PAC, bool FULL>
+static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
+    switch (p.N) {
+        case 4: return launch_t<4, 4, PAC, FULL>(p, a, s);
+        case 8: return launch_t<8, 8, PAC, FULL>(p, a, s);
+        case 16: return launch_t<16, 16, PAC, FULL>(p, a, s);
+        case 32: return launch_t<32, 32, PAC, FULL>(p, a, s);
+        case 64: return launch_t<64, 64, PAC, FULL>(p, a, s);
+        case 128: return launch_t<128, 64, PAC, FULL>(p, a, s);
+        case 256: return launch_t<256, 64, PAC, FULL>(p, a, s);
+        default: return fail(NPD_EINVAL, "sc_decode: unsupported N");
+    }
+}
+
+static int run(const npd_code* code, Args a, hipStream_t s) {
+    if (a.B == 0) return NPD_OK;
+    const bool full = (a.flags & (kLeaf | kGt | kUhat)) != 0;
+    if (code->p.pac) return full ? dispatch<true, true>(code->p, a, s) : dispatch<true, false>(code->p, a, s);
+    return full ? dispatch<false, true>(code->p, a, s) : dispatch<false, false>(code->p, a, s);
+}
+
+}  // namespace sc
+}  // namespace npd
+
+using namespace npd;
+
+extern "C" int npd_sc_decode(const npd_code* code, const float* y, float llr_scale, float* leaf_llr, float* msg_hat,
+                             float* u_hat, const float* gt, int64_t B, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_decode: code is NULL");
+    NPD_ARG(B >= 0, "npd_sc_decode: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode: y is NULL");
+    NPD_ARG(code->p.pac || u_hat == nullptr, "npd_sc_decode: u_hat is only produced for PAC codes");
+    sc::Args a{};
+    a.y = y;
+    a.leaf = leaf_llr;
+    a.msg = msg_hat;
+    a.uhat = u_hat;
+    a.gt = gt;
+    a.B = B;
+    a.scale = llr_scale;
+    a.flags = (leaf_llr ? sc::kLeaf : 0u) | (msg_hat ? sc::kMsg : 0u) | (u_hat ? sc::kUhat : 0u) | (gt ? sc::kGt : 0u);
+    return sc::run(code, a, (hipStream_t)stream);
+}
+
+extern "C" int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_scale, float* msg_hat, uint64_t seed,
+                                uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_decode_mc: code is NULL");
+    NPD_ARG(B >= 0, "npd_sc_decode_mc: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_mc: y is NULL");
+    NPD_ARG(counters != nullptr, "npd_sc_decode_mc: counters is NULL");
+    sc::Args a{};
+    a.y = y;
+    a.msg = msg_hat;
+    a.counters = counters;
+    a.seed = seed;
+    a.cw_offset = cw_offset;
+    a.B = B;
+    a.scale = llr_scale;
+    a.flags = sc::kCount | (msg_hat ? sc::kMsg : 0u);
+    return sc::run(code, a, (hipStream_t)stream);
+}

@@ -1,0 +1,194 @@
+"""PolarCode -- drop-in for the reference's ``polar.PolarCode`` hot-path surface (polar.py:64-484).
+
+Same constructor and method signatures as the reference; every compute method runs on the MI355X
+through libnpd (HIP kernels, ctypes C-ABI).  Tensors must live on the GPU.
+
+  PolarCode(n, K, args=None, F=None, rs=None, use_cuda=True, infty=1000.)      polar.py:66-117
+  .encode_plotkin(message, scaling=None, custom_info_positions=None)            polar.py:128-148
+  .encode  (alias of encode_plotkin, as rnn_all.get_code sets it, rnn_all.py:1187)
+  .channel(code, snr)                                                           polar.py:201-207
+  .sc_decode_new(corrupted_codewords, snr, use_gt=None) -> (leaf_llrs, msg_hat) polar.py:465-484
+
+MI355X extras (no reference equivalent, used by the Monte-Carlo driver and bench):
+  .mc_generate(B, snr, seed, snr_index, cw_offset)   fused msg -> encode -> AWGN on device
+  .sc_decode_mc(y, snr, seed, cw_offset, counters)   decode + fused error counting
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib
+from .codes import info_from_frozen, polar_rs
+from .utils import llr_scale, sigma_f32, snr_db2sigma
+
+
+class _CodeHandle:
+    """Owns one npd_code (immutable once created)."""
+
+    def __init__(self, N: int, info: np.ndarray, pac_g: int = 0, infty: float = 1000.0):
+        L = _lib.load()
+        info32 = np.ascontiguousarray(np.sort(np.asarray(info, dtype=np.int64)), dtype=np.int32)
+        out = ctypes.c_void_p()
+        _lib.check(L.npd_code_create(int(N), int(info32.size), info32.ctypes.data_as(ctypes.c_void_p), int(pac_g),
+                                     float(infty), ctypes.byref(out)), "npd_code_create")
+        self.h = out
+        self.N = int(N)
+        self.K = int(info32.size)
+        self.info = info32.astype(np.int64)
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.load().npd_code_destroy(self.h)
+        except Exception:
+            pass
+
+
+class _Philox:
+    """Host-side bookkeeping for the counter-based channel RNG: (seed, running codeword offset)."""
+
+    def __init__(self, seed=None):
+        self.seed = int(torch.initial_seed() if seed is None else seed) & 0xFFFFFFFFFFFFFFFF
+        self.offset = 0
+        self.lock = threading.Lock()
+
+    def take(self, n):
+        with self.lock:
+            o = self.offset
+            self.offset += int(n)
+        return o
+
+
+class PolarCode:
+    def __init__(self, n, K, args=None, F=None, rs=None, use_cuda=True, infty=1000.):
+        assert n >= 1
+        self.args = args
+        self.n = n
+        self.N = 2 ** n
+        self.K = K
+        self.infty = infty
+        self.device = torch.device("cuda" if use_cuda else "cpu")
+        if F is not None:
+            assert len(F) == self.N - self.K
+            self.frozen_positions = np.sort(np.asarray(F))
+            self.unsorted_frozen_positions = np.asarray(F)
+            self.info_positions = info_from_frozen(self.N, F)
+            self.unsorted_info_positions = self.info_positions
+        else:
+            if rs is None:
+                self.reliability_seq = np.arange(1023, -1, -1)
+            else:
+                self.reliability_seq = np.asarray(rs)
+            self.rs = self.reliability_seq[self.reliability_seq < self.N]
+            if rs is not None:
+                assert len(self.rs) == self.N
+            self.unsorted_info_positions = np.flip(self.rs[:self.K].copy())
+            self.info_positions = np.sort(self.rs[:self.K].copy())
+            self.unsorted_frozen_positions = self.rs[self.K:].copy()
+            self.frozen_positions = np.sort(self.rs[self.K:].copy())
+        self._code = None
+        self._custom = {}
+        self._rng = _Philox()
+
+    # ------------------------------------------------------------------ handles
+    @property
+    def code(self) -> _CodeHandle:
+        if self._code is None:
+            self._code = _CodeHandle(self.N, self.info_positions, 0, self.infty)
+        return self._code
+
+    def _code_for(self, info_positions) -> _CodeHandle:
+        if info_positions is None:
+            return self.code
+        key = tuple(int(i) for i in np.sort(np.asarray(info_positions)))
+        h = self._custom.get(key)
+        if h is None:
+            h = self._custom[key] = _CodeHandle(self.N, np.asarray(key), 0, self.infty)
+        return h
+
+    def manual_seed(self, seed: int):
+        """Seed the channel's Philox stream (the reference draws torch.randn on the CPU generator)."""
+        self._rng = _Philox(seed)
+
+    # ------------------------------------------------------------------ encoder (polar.py:128-148)
+    def encode_plotkin(self, message, scaling=None, custom_info_positions=None):
+        _lib.require_gpu(message, "message")
+        h = self._code_for(custom_info_positions)
+        msg = _lib.f32c(message)
+        if msg.dim() != 2 or msg.shape[1] != h.K:
+            raise ValueError(f"message must be (batch, {h.K}), got {tuple(msg.shape)}")
+        x = torch.empty(msg.shape[0], self.N, dtype=torch.float32, device=msg.device)
+        _lib.check(_lib.load().npd_encode(h.h, _lib.ptr(msg), _lib.ptr(x), msg.shape[0], _lib.stream_of(msg.device)),
+                   "npd_encode")
+        if scaling is not None:
+            x = (scaling * np.sqrt(self.N) * x) / torch.norm(scaling)
+        return x
+
+    encode = encode_plotkin
+
+    # ------------------------------------------------------------------ channel (polar.py:201-207)
+    def channel(self, code, snr, snr_index: int = 0):
+        _lib.require_gpu(code, "code")
+        x = _lib.f32c(code)
+        B, N = x.shape
+        y = torch.empty_like(x)
+        off = self._rng.take(B)
+        _lib.check(_lib.load().npd_awgn(_lib.ptr(x), _lib.ptr(y), B, N, sigma_f32(snr), self._rng.seed, int(snr_index),
+                                        off, _lib.stream_of(x.device)), "npd_awgn")
+        return y
+
+    # ------------------------------------------------------------------ SC (polar.py:465-484)
+    def sc_decode_new(self, corrupted_codewords, snr, use_gt=None):
+        """Min-sum SC; returns (leaf LLRs incl. the frozen prior (B,N), msg_hat (B,K)) bit-exactly."""
+        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
+        y = _lib.f32c(corrupted_codewords)
+        B = y.shape[0]
+        leaf = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
+        hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
+        gt = None if use_gt is None else _lib.f32c(use_gt.to(y.device))
+        _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(leaf), _lib.ptr(hat), None,
+                                             _lib.ptr(gt), B, _lib.stream_of(y.device)), "npd_sc_decode")
+        return leaf, hat
+
+    def sc_decode_msg(self, corrupted_codewords, snr):
+        """msg_hat only (no leaf LLR traffic): the form the BER/BLER loops consume."""
+        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
+        y = _lib.f32c(corrupted_codewords)
+        hat = torch.empty(y.shape[0], self.K, dtype=torch.float32, device=y.device)
+        _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), None, _lib.ptr(hat), None, None,
+                                             y.shape[0], _lib.stream_of(y.device)), "npd_sc_decode")
+        return hat
+
+    # The reference's ``sc_decode`` (polar.py:209-279) is a different (exact-LSE, soft) decoder that
+    # the eval loops do not call; out of scope here.
+
+    # ------------------------------------------------------------------ Monte-Carlo extras
+    def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False):
+        device = torch.device(device or "cuda")
+        y = torch.empty(B, self.N, dtype=torch.float32, device=device)
+        msg = torch.empty(B, self.K, dtype=torch.float32, device=device) if want_msg else None
+        x = torch.empty(B, self.N, dtype=torch.float32, device=device) if want_x else None
+        _lib.check(_lib.load().npd_mc_generate(self.code.h, _lib.ptr(msg), _lib.ptr(x), _lib.ptr(y), B, sigma_f32(snr),
+                                               int(seed), int(snr_index), int(cw_offset), _lib.stream_of(device)),
+                   "npd_mc_generate")
+        return msg, x, y
+
+    def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
+        _lib.require_gpu(y, "y")
+        _lib.check(_lib.load().npd_sc_decode_mc(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(msg_hat), int(seed),
+                                                int(cw_offset), y.shape[0], _lib.ptr(counters), _lib.stream_of(y.device)),
+                   "npd_sc_decode_mc")
+        return counters
+
+
+def reference_polar_code(N: int, K: int, args=None, infty=1000.) -> PolarCode:
+    """PolarCode(n, K, args, rs=rs) with the reference's 'polar' reliability order (run_models.py:630-639)."""
+    n = int(np.log2(N))
+    return PolarCode(n, K, args, rs=polar_rs(N), infty=infty)
+
+
+__all__ = ["PolarCode", "reference_polar_code", "snr_db2sigma"]

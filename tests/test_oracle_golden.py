@@ -1,0 +1,128 @@
+"""CPU: the oracle (oracle/npd_oracle.c + oracle.py) against the reference's golden vectors, and the
+host-side code construction against the reference's information sets."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+SC_CASES = [(32, 16), (64, 32), (128, 64), (256, 128), (16, 8), (64, 22)]
+PAC_CASES = [(128, 64), (64, 22), (32, 16)]
+
+
+def test_encode_plotkin_golden(oracle):
+    e = golden("encode.npz")
+    for N, K in [(32, 16), (64, 32), (128, 64), (256, 128), (8, 4)]:
+        x = oracle.encode_plotkin(e[f"msg_{N}_{K}"], N, e[f"info_{N}_{K}"])
+        assert np.array_equal(x, e[f"x_{N}_{K}"]), N
+    x = oracle.encode_plotkin(e["msgf_16_8"], 16, e["info_16_8"])  # non +-1 messages: product order
+    assert np.array_equal(x, e["xf_16_8"])
+
+
+def test_pac_encode_golden(oracle):
+    e = golden("encode.npz")
+    for N, K in PAC_CASES:
+        x = oracle.pac_encode(e[f"pmsg_{N}_{K}"], N, e[f"pinfo_{N}_{K}"])
+        assert np.array_equal(x, e[f"px_{N}_{K}"]), N
+
+
+@pytest.mark.parametrize("N,K", SC_CASES)
+def test_sc_decode_golden(oracle, N, K):
+    d = golden(f"sc_polar_{N}_{K}.npz")
+    for s in np.unique(d["snr"]):
+        m = d["snr"] == s
+        leaf, hat = oracle.sc_decode(d["y"][m], float(s), d["info"])
+        assert np.array_equal(leaf, d["leaf"][m])
+        assert np.array_equal(hat, d["msg_hat"][m])
+    gl, gh = oracle.sc_decode(d["gt_y"], float(d["gt_snr"]), d["info"], gt=d["gt"])
+    assert np.array_equal(gl, d["gt_leaf"]) and np.array_equal(gh, d["gt_msg_hat"])
+
+
+@pytest.mark.parametrize("N,K", PAC_CASES)
+def test_pac_sc_decode_golden(oracle, N, K):
+    d = golden(f"sc_pac_{N}_{K}.npz")
+    for s in np.unique(d["snr"]):
+        m = d["snr"] == s
+        leaf, hat, uh = oracle.pac_sc_decode(d["y"][m], float(s), d["info"])
+        assert np.array_equal(leaf, d["leaf"][m])
+        assert np.array_equal(hat, d["msg_hat"][m])
+        assert np.array_equal(uh, d["u_hat"][m])
+    gl, gh, gu = oracle.pac_sc_decode(d["gt_y"], float(d["gt_snr"]), d["info"], gt=d["gt"])
+    assert np.array_equal(gl, d["gt_leaf"]) and np.array_equal(gh, d["gt_msg_hat"]) and np.array_equal(gu, d["gt_u_hat"])
+
+
+def test_error_counters_golden(oracle):
+    d = golden("errors.npz")
+    be, bl = oracle.count_errors(d["ref"], d["hat"])
+    assert be / d["ref"].size == pytest.approx(float(d["ber"]), abs=0)
+    assert bl / d["ref"].shape[0] == pytest.approx(float(d["bler"]), abs=0)
+
+
+@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev"])
+def test_gru_oracle_golden(oracle, name):
+    d = golden(f"{name}.npz")
+    sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    dec, lg = oracle.gru_decode(d["y"], sd, int(d["N"]), int(d["F"]), 2, d["info"], onehot=bool(d["onehot"]),
+                                rev=bool(d["rev"]), want_logits=True)
+    assert np.abs(lg - d["logits"]).max() < 1e-5
+    assert (dec == d["decoded"]).mean() > 0.9999
+
+
+def test_conv_oracle_golden(oracle):
+    d = golden("conv_small_64.npz")
+    sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    lg = oracle.conv_forward(d["y"], sd)
+    assert np.abs(lg - d["logits"]).max() < 1e-5
+
+
+def test_conv_seed_generator_matches_golden_c5(oracle):
+    """The C5 fixture's weights are regenerated from the documented seed (not stored)."""
+    from conftest import conv_weights_from_seed
+    d = golden("conv_c5_256.npz")
+    sd = conv_weights_from_seed(int(d["embed"]), int(d["N"]), int(d["seed"]))
+    lg = oracle.conv_forward(d["y"][:4], sd)
+    assert np.abs(lg - d["logits"][:4]).max() < 1e-4
+
+
+def test_info_sets_match_reference():
+    from neural_polar_decoder_amd.codes import pac_info_positions, polar_info_positions
+    d = golden("codes.npz")
+    for key in d.files:
+        parts = key.split("_")
+        if parts[0] == "polar":
+            prof = "_".join(parts[1:-3])
+            N, K, tK = (int(v) for v in parts[-3:])
+            got = polar_info_positions(N, K, prof, target_K=tK, random_seed=42)
+        else:
+            N, K = int(parts[-2]), int(parts[-1])
+            got = pac_info_positions(N, K, "RM", target_K=K)
+        assert np.array_equal(got, np.sort(d[key])), key
+
+
+def test_philox_msg_stream_known_answer(oracle):
+    # Philox4x32-10 known-answer vector (Random123 kat_vectors: ctr=0, key=0)
+    import ctypes
+    L = oracle.lib()
+    out = (ctypes.c_uint32 * 4)()
+    ctr = (ctypes.c_uint32 * 4)(0, 0, 0, 0)
+    key = (ctypes.c_uint32 * 2)(0, 0)
+    L.oracle_philox4x32_10(ctr, key, out)
+    assert list(out) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    ctr = (ctypes.c_uint32 * 4)(0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF)
+    key = (ctypes.c_uint32 * 2)(0xFFFFFFFF, 0xFFFFFFFF)
+    L.oracle_philox4x32_10(ctr, key, out)
+    assert list(out) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+def test_oracle_mc_is_generate_then_decode(oracle):
+    """Fused CPU MC == gen_msg -> encode -> awgn -> sc_decode -> count (same Philox streams)."""
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    N, K = 64, 32
+    info = polar_info_positions(N, K)
+    B, seed = 2048, 1234
+    for si, snr in enumerate([0.0, 2.0]):
+        msg = oracle.gen_msg(B, K, seed, 4096)
+        x = oracle.encode_plotkin(msg, N, info)
+        y = oracle.awgn(x, snr, seed, si, 4096)
+        _, hat = oracle.sc_decode(y, snr, info)
+        be, bl = oracle.count_errors(msg, hat)
+        assert (be, bl) == oracle.mc_sc(B, N, info, snr, seed, si, cw_offset=4096)

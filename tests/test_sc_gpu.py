@@ -1,0 +1,232 @@
+"""GPU parity: encoder, channel, SC / PAC-SC decoders and counters through the C-ABI
+(neural_polar_decoder_amd -> libnpd.so) against the reference's golden vectors and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+SC_CASES = [(32, 16), (64, 32), (128, 64), (256, 128), (16, 8), (64, 22)]
+PAC_CASES = [(128, 64), (64, 22), (32, 16)]
+DEV = "cuda:0"
+
+
+def polar_for(N, info):
+    from neural_polar_decoder_amd import PolarCode
+    n = int(np.log2(N))
+    K = len(info)
+    F = np.array(sorted(set(range(N)) - set(int(i) for i in info)))
+    return PolarCode(n, K, F=F)
+
+
+def pac_for(N, K):
+    import argparse
+    from neural_polar_decoder_amd import PAC
+    return PAC(argparse.Namespace(target_K=K), N, K, 91)
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def test_encode_plotkin_golden():
+    e = golden("encode.npz")
+    for N, K in [(32, 16), (64, 32), (128, 64), (256, 128), (8, 4)]:
+        code = polar_for(N, e[f"info_{N}_{K}"])
+        x = code.encode_plotkin(t(e[f"msg_{N}_{K}"])).cpu().numpy()
+        assert np.array_equal(x, e[f"x_{N}_{K}"]), N
+    code = polar_for(16, e["info_16_8"])
+    assert np.array_equal(code.encode_plotkin(t(e["msgf_16_8"])).cpu().numpy(), e["xf_16_8"])
+
+
+def test_pac_encode_golden():
+    e = golden("encode.npz")
+    for N, K in PAC_CASES:
+        pac = pac_for(N, K)
+        assert np.array_equal(pac.B, e[f"pinfo_{N}_{K}"])
+        x = pac.pac_encode(t(e[f"pmsg_{N}_{K}"]), scheme="RM").cpu().numpy()
+        assert np.array_equal(x, e[f"px_{N}_{K}"]), N
+
+
+@pytest.mark.parametrize("N,K", SC_CASES)
+def test_sc_decode_golden(N, K):
+    d = golden(f"sc_polar_{N}_{K}.npz")
+    code = polar_for(N, d["info"])
+    for s in np.unique(d["snr"]):
+        m = d["snr"] == s
+        leaf, hat = code.sc_decode_new(t(d["y"][m]), float(s))
+        assert np.array_equal(leaf.cpu().numpy(), d["leaf"][m]), (N, s)
+        assert np.array_equal(hat.cpu().numpy(), d["msg_hat"][m]), (N, s)
+        hat2 = code.sc_decode_msg(t(d["y"][m]), float(s))  # fast (msg-only) kernel variant
+        assert np.array_equal(hat2.cpu().numpy(), d["msg_hat"][m]), (N, s)
+    gl, gh = code.sc_decode_new(t(d["gt_y"]), float(d["gt_snr"]), use_gt=t(d["gt"]))
+    assert np.array_equal(gl.cpu().numpy(), d["gt_leaf"]) and np.array_equal(gh.cpu().numpy(), d["gt_msg_hat"])
+
+
+@pytest.mark.parametrize("N,K", PAC_CASES)
+def test_pac_sc_decode_golden(N, K):
+    d = golden(f"sc_pac_{N}_{K}.npz")
+    pac = pac_for(N, K)
+    for s in np.unique(d["snr"]):
+        m = d["snr"] == s
+        leaf, hat, uh = pac.pac_sc_decode(t(d["y"][m]), float(s))
+        assert np.array_equal(leaf.cpu().numpy(), d["leaf"][m])
+        assert np.array_equal(hat.cpu().numpy(), d["msg_hat"][m])
+        assert np.array_equal(uh.cpu().numpy(), d["u_hat"][m])
+    gl, gh, gu = pac.pac_sc_decode(t(d["gt_y"]), float(d["gt_snr"]), use_gt_codeword=t(d["gt"]))
+    assert np.array_equal(gl.cpu().numpy(), d["gt_leaf"])
+    assert np.array_equal(gh.cpu().numpy(), d["gt_msg_hat"])
+    assert np.array_equal(gu.cpu().numpy(), d["gt_u_hat"])
+
+
+@pytest.mark.parametrize("N,K", [(4, 2), (8, 4), (16, 8), (32, 16), (64, 32), (128, 64), (256, 128), (64, 1), (64, 64)])
+def test_sc_decode_vs_oracle_random(oracle, N, K):
+    """Ragged batch sizes (tails of the 64-codeword tiles), all code lengths, edge rates."""
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    info = polar_info_positions(N, K)
+    code = polar_for(N, info)
+    rng = np.random.default_rng(N * 131 + K)
+    for B in (1, 63, 65, 1000):
+        y = (rng.standard_normal((B, N)) + (1 - 2 * (rng.random((B, N)) < 0.5))).astype(np.float32)
+        leaf, hat = code.sc_decode_new(t(y), 1.5)
+        ol, oh = oracle.sc_decode(y, 1.5, info)
+        assert np.array_equal(leaf.cpu().numpy(), ol) and np.array_equal(hat.cpu().numpy(), oh), B
+
+
+def test_pac_vs_oracle_random(oracle):
+    pac = pac_for(128, 64)
+    rng = np.random.default_rng(3)
+    y = rng.standard_normal((777, 128)).astype(np.float32)
+    leaf, hat, uh = pac.pac_sc_decode(t(y), 0.5)
+    ol, oh, ou = oracle.pac_sc_decode(y, 0.5, pac.B)
+    assert np.array_equal(leaf.cpu().numpy(), ol)
+    assert np.array_equal(hat.cpu().numpy(), oh)
+    assert np.array_equal(uh.cpu().numpy(), ou)
+
+
+def test_channel_statistics():
+    from neural_polar_decoder_amd import reference_polar_code
+    code = reference_polar_code(64, 32)
+    code.manual_seed(7)
+    x = torch.ones(1 << 16, 64, device=DEV)
+    for snr in (0.0, 3.0):
+        y = code.channel(x, snr)
+        n = (y - x).double()
+        sigma = 10 ** (-snr / 20)
+        assert abs(n.mean().item()) < 5e-3 * sigma
+        assert abs(n.std().item() / sigma - 1) < 5e-3
+    y1, y2 = code.channel(x, 1.0), code.channel(x, 1.0)
+    assert not torch.equal(y1, y2)  # the counter advances between calls
+
+
+def test_awgn_matches_oracle(oracle):
+    rng = np.random.default_rng(9)
+    x = (1 - 2 * (rng.random((333, 64)) < 0.5)).astype(np.float32)
+    from neural_polar_decoder_amd import _lib
+    from neural_polar_decoder_amd.utils import sigma_f32
+    xd = t(x)
+    y = torch.empty_like(xd)
+    _lib.check(_lib.load().npd_awgn(_lib.ptr(xd), _lib.ptr(y), 333, 64, sigma_f32(2.0), 99, 3, 1000,
+                                    _lib.stream_of(xd.device)))
+    yo = oracle.awgn(x, 2.0, 99, 3, 1000)
+    assert np.abs(y.cpu().numpy() - yo).max() < 2e-5
+
+
+@pytest.mark.parametrize("N,K,pac", [(64, 32, False), (32, 16, False), (256, 128, False), (128, 64, True)])
+def test_mc_generate_matches_oracle(oracle, N, K, pac):
+    if pac:
+        code = pac_for(N, K)
+        info = code.B
+    else:
+        from neural_polar_decoder_amd import reference_polar_code
+        code = reference_polar_code(N, K)
+        info = code.info_positions
+    msg, x, y = code.mc_generate(2000, 1.0, seed=1234, snr_index=2, cw_offset=777, want_msg=True, want_x=True)
+    om = oracle.gen_msg(2000, K, 1234, 777)
+    assert np.array_equal(msg.cpu().numpy(), om)
+    ox = oracle.pac_encode(om, N, info) if pac else oracle.encode_plotkin(om, N, info)
+    assert np.array_equal(x.cpu().numpy(), ox)
+    oy = oracle.awgn(ox, 1.0, 1234, 2, 777)
+    assert np.abs(y.cpu().numpy() - oy).max() < 2e-5
+
+
+@pytest.mark.parametrize("N,K,pac", [(64, 32, False), (32, 16, False), (128, 64, False), (256, 128, False),
+                                     (128, 64, True), (64, 22, True)])
+def test_sc_decode_mc_counters_exact(oracle, N, K, pac):
+    """Fused decode+count on GPU-generated y == oracle decode + count on the same y (bit-exact)."""
+    if pac:
+        code = pac_for(N, K)
+        info = code.B
+    else:
+        from neural_polar_decoder_amd import reference_polar_code
+        code = reference_polar_code(N, K)
+        info = code.info_positions
+    B, seed, off = 5000, 42, 12345
+    for si, snr in enumerate([0.0, 2.0, 4.0]):
+        msg, _, y = code.mc_generate(B, snr, seed, si, off)
+        cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+        hat = torch.empty(B, K, device=DEV)
+        code.sc_decode_mc(y, snr, seed, off, cnt, msg_hat=hat)
+        yh = y.cpu().numpy()
+        if pac:
+            _, oh, _ = oracle.pac_sc_decode(yh, snr, info)
+        else:
+            _, oh = oracle.sc_decode(yh, snr, info)
+        assert np.array_equal(hat.cpu().numpy(), oh)
+        be, bl = oracle.count_errors(msg.cpu().numpy(), oh)
+        assert cnt.cpu().tolist() == [be, bl], (snr, cnt.cpu().tolist(), be, bl)
+
+
+def test_count_errors_golden():
+    from neural_polar_decoder_amd import errors_ber, errors_bler
+    d = golden("errors.npz")
+    assert float(errors_ber(t(d["ref"]), t(d["hat"]))) == pytest.approx(float(d["ber"]), abs=0)
+    assert errors_bler(t(d["ref"]), t(d["hat"])) == pytest.approx(float(d["bler"]), abs=0)
+
+
+def test_full_size_properties():
+    """B = 2^20 (config C2): noiseless round trip, shard invariance, counters == separate count."""
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.utils import count_errors
+    code = reference_polar_code(64, 32)
+    B = 1 << 20
+    msg, x, y = code.mc_generate(B, 2.0, seed=5, snr_index=0, cw_offset=0, want_x=True)
+    # noiseless: decoding the clean codeword returns the message exactly (every bit, every codeword)
+    hat = code.sc_decode_msg(x, 2.0)
+    assert torch.equal(hat, msg)
+    # decode + fused count == decode then separate count
+    cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+    hat = torch.empty(B, 32, device=DEV)
+    code.sc_decode_mc(y, 2.0, 5, 0, cnt, msg_hat=hat)
+    assert torch.equal(hat, code.sc_decode_msg(y, 2.0))
+    c2 = count_errors(msg, hat)
+    assert torch.equal(cnt, c2)
+    # sharding invariance: two half launches with offsets == one launch
+    c3 = torch.zeros(2, dtype=torch.int64, device=DEV)
+    code.sc_decode_mc(y[: B // 2], 2.0, 5, 0, c3)
+    code.sc_decode_mc(y[B // 2:], 2.0, 5, B // 2, c3)
+    assert torch.equal(cnt, c3)
+
+
+def test_ber_curve_matches_reference_anchors():
+    """SC BER/BLER at 2^20 codewords/SNR vs the reference's anchors (BASELINE.md, 1e5 cw/SNR, torch RNG):
+    agreement within 4 combined standard errors (binomial, block-level for BER)."""
+    from neural_polar_decoder_amd import reference_polar_code
+    anchors = {0: (1.944e-1, 5.664e-1), 1: (9.996e-2, 3.166e-1), 2: (3.634e-2, 1.248e-1),
+               3: (8.425e-3, 3.116e-2), 4: (1.258e-3, 4.910e-3)}
+    code = reference_polar_code(64, 32)
+    B = 1 << 20
+    for si, (snr, (ber_ref, bler_ref)) in enumerate(anchors.items()):
+        _, _, y = code.mc_generate(B, float(snr), seed=1234, snr_index=si, cw_offset=0, want_msg=False)
+        cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+        code.sc_decode_mc(y, float(snr), 1234, 0, cnt)
+        be, bl = cnt.cpu().tolist()
+        bler = bl / B
+        ber = be / (B * 32)
+        se_bler = np.sqrt(bler_ref * (1 - bler_ref) * (1 / 1e5 + 1 / B))
+        assert abs(bler - bler_ref) < 4 * se_bler + 1e-12, (snr, bler, bler_ref)
+        # bit errors cluster within blocks: bound with the block-level variance of errors per block
+        se_ber = np.sqrt((1 / 1e5 + 1 / B)) * np.sqrt(bler_ref) * (ber_ref / max(bler_ref, 1e-9)) * 2.5
+        assert abs(ber - ber_ref) < 4 * se_ber + 1e-12, (snr, ber, ber_ref)
