@@ -47,6 +47,14 @@ struct Args {
 };
 
 // ------------------------------------------------------------------------------ small helpers
+// The reference rounds L = fl32(scale*y) before any add (polar.py:468).  hipcc contracts fmul+fadd
+// into fma by default, even for __fmul_rn; an empty asm makes the rounded product opaque.
+__device__ __forceinline__ float rmul(float a, float b) {
+    float r = a * b;
+    asm("" : "+v"(r));
+    return r;
+}
+
 __device__ __forceinline__ float f_minsum(float a, float b) {
     const float m = __builtin_fminf(__builtin_fabsf(a), __builtin_fabsf(b));
     return bitsf(fbits(m) | ((fbits(a) ^ fbits(b)) & 0x80000000u));
@@ -72,8 +80,9 @@ __device__ __forceinline__ int swz(int r) {
 
 template <int N>
 struct Geo {
-    static constexpr int C = N / 4;  // 16-B chunks per row
-    static constexpr int NP = N + 1; // padded row stride (floats) for per-lane rows
+    static constexpr int C = N / 4;             // 16-B chunks per row
+    static constexpr int NP = N + 1;            // padded row stride (floats) for per-lane float rows
+    static constexpr int NB = 4 * ((N / 4) | 1);  // byte-row stride: an odd number of dwords (conflict-free)
 };
 
 // ------------------------------------------------------------------------------ per-lane context
@@ -88,7 +97,10 @@ struct Ctx {
     char* lds;
     uint32_t stage_row;   // staging chunk base for this lane's row (chunk index r*C)
     int sw;               // this lane's swizzle
-    uint32_t u_row, v_row, leaf_row, gt_row;
+    uint32_t u_row, v_row;            // decision rows (int8 per position, stride NB bytes)
+    uint32_t leaf_row, gt_row;        // float rows (R == N only; stride N+1 floats)
+    float* leaf_g;                    // R < N: this lane's leaf-LLR output row in HBM (or null)
+    const float* gt_g;                // R < N: this lane's genie row in HBM (or null)
     uint32_t lvl_row[9];  // per-level LDS rows for upper levels (node size > R, < N)
     float scale;
     uint32_t flags;
@@ -102,32 +114,54 @@ __device__ __forceinline__ float4 stage_chunk(char* lds, uint32_t off_stage, uin
 
 __device__ __forceinline__ void lds_wr(char* lds, uint32_t byte, float v) { *reinterpret_cast<float*>(lds + byte) = v; }
 __device__ __forceinline__ float lds_rd(const char* lds, uint32_t byte) { return *reinterpret_cast<const float*>(lds + byte); }
+__device__ __forceinline__ void lds_wr8(char* lds, uint32_t byte, float v) {
+    *reinterpret_cast<int8_t*>(lds + byte) = (int8_t)(int)v;  // v in {-1, 0, 1}
+}
+__device__ __forceinline__ float lds_rd8(const char* lds, uint32_t byte) {
+    return (float)*reinterpret_cast<const int8_t*>(lds + byte);
+}
 
 // ------------------------------------------------------------------------------ leaf
 template <int N, int R, bool PAC, bool FULL, int I>
+__device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL>& c, float v) {
+    if constexpr (FULL) {
+        if (c.flags & kLeaf) {
+            if constexpr (R == N) lds_wr(c.lds, c.leaf_row + 4 * I, v);
+            else c.leaf_g[I] = v;
+        }
+    }
+}
+
+template <int N, int R, bool PAC, bool FULL, int I>
+__device__ __forceinline__ float genie(const Ctx<N, R, PAC, FULL>& c) {
+    if constexpr (R == N) return lds_rd(c.lds, c.gt_row + 4 * I);
+    else return c.gt_g[I];
+}
+
+template <int N, int R, bool PAC, bool FULL, int I>
 __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a, float L) {
     const bool frozen = (p.frozen[I >> 5] >> (I & 31)) & 1u;
+    const bool use_gt = FULL && (c.flags & kGt);
     float u;
     if constexpr (!PAC) {
         // polar.py:438/446: leaf = L + prior; prior = infty on frozen positions, 0 elsewhere
         const float lf = L + (frozen ? p.infty : 0.0f);
-        if (FULL && (c.flags & kLeaf)) lds_wr(c.lds, c.leaf_row + 4 * I, lf);
-        if (FULL && (c.flags & kGt)) u = lds_rd(c.lds, c.gt_row + 4 * I);
-        else u = sgn_bits(lf);
+        write_leaf<N, R, PAC, FULL, I>(c, lf);
+        u = use_gt ? genie<N, R, PAC, FULL, I>(c) : sgn_bits(lf);
     } else {
-        if (FULL && (c.flags & kLeaf)) lds_wr(c.lds, c.leaf_row + 4 * I, L);
+        write_leaf<N, R, PAC, FULL, I>(c, L);
         const float u0 = (__builtin_popcount(c.st & p.tapmask) & 1) ? -1.0f : 1.0f;  // conv(+1) (pac_code.py:188-193)
         float v;
         if (frozen) {  // pac_code.py:545-551
             v = 1.0f;
-            if (FULL && (c.flags & kGt)) {
-                u = lds_rd(c.lds, c.gt_row + 4 * I);
+            if (use_gt) {
+                u = genie<N, R, PAC, FULL, I>(c);
             } else {
                 u = u0;
                 c.st = (c.st << 1) & p.smask;
             }
         } else {  // pac_code.py:553-568
-            u = (FULL && (c.flags & kGt)) ? lds_rd(c.lds, c.gt_row + 4 * I) : sgn_bits(L);
+            u = use_gt ? genie<N, R, PAC, FULL, I>(c) : sgn_bits(L);
             if (u == u0) {
                 v = 1.0f;
                 c.st = (c.st << 1) & p.smask;
@@ -138,9 +172,9 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& 
                 v = 0.0f;
             }
         }
-        lds_wr(c.lds, c.v_row + 4 * I, v);
+        lds_wr8(c.lds, c.v_row + I, v);
     }
-    lds_wr(c.lds, c.u_row + 4 * I, u);
+    lds_wr8(c.lds, c.u_row + I, u);
     c.beta[I % R] = u;
 }
 
@@ -193,7 +227,7 @@ __device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL>& c, const Arg
     if constexpr ((1 << D) == N) {
         // staging: element j of the row is in chunk j/4, sub j%4
         const uint32_t addr = a.off_stage + ((c.stage_row + (uint32_t)((j >> 2) ^ c.sw)) << 4) + 4 * (j & 3);
-        return c.scale * lds_rd(c.lds, addr);
+        return rmul(c.scale, lds_rd(c.lds, addr));
     } else {
         return lds_rd(c.lds, c.lvl_row[D] + 4 * j);
     }
@@ -218,10 +252,10 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
             for (int q = 0; q < h / 4; ++q) {
                 const float4 A = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q);
                 const float4 Bv = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q + h / 4);
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 0, f_minsum(c.scale * A.x, c.scale * Bv.x));
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 1, f_minsum(c.scale * A.y, c.scale * Bv.y));
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 2, f_minsum(c.scale * A.z, c.scale * Bv.z));
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 3, f_minsum(c.scale * A.w, c.scale * Bv.w));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 0, f_minsum(rmul(c.scale, A.x), rmul(c.scale, Bv.x)));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 1, f_minsum(rmul(c.scale, A.y), rmul(c.scale, Bv.y)));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 2, f_minsum(rmul(c.scale, A.z), rmul(c.scale, Bv.z)));
+                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 3, f_minsum(rmul(c.scale, A.w), rmul(c.scale, Bv.w)));
             }
         } else {
 #pragma unroll
@@ -240,7 +274,7 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
                 for (int e = 0; e < 4; ++e) {
                     const int pos = S0 + 4 * q + e;
                     up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + e,
-                                             g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, c.scale * av[e], c.scale * bv[e]));
+                                             g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
                 }
             }
         } else {
@@ -272,6 +306,7 @@ constexpr int log2c() {
 
 // ------------------------------------------------------------------------------ output pass
 // store W floats per row for the tile's `rows` valid rows: value(r, col) = lds[base + r*stride + 4*map(col)]
+template <bool BYTES>
 __device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint32_t stride_b, const int32_t* info_lds,
                                            int W, float* out, int64_t tile_row0, int rows, int lane) {
     if (out == nullptr || W == 0) return;
@@ -281,7 +316,8 @@ __device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint3
     const int dr = kWave / W, dc = kWave % W;
     for (int e = lane; e < total; e += kWave) {
         const int m = info_lds ? info_lds[col] : col;
-        dst[e] = lds_rd(lds, base + (uint32_t)r * stride_b + 4u * (uint32_t)m);
+        if constexpr (BYTES) dst[e] = lds_rd8(lds, base + (uint32_t)r * stride_b + (uint32_t)m);
+        else dst[e] = lds_rd(lds, base + (uint32_t)r * stride_b + 4u * (uint32_t)m);
         r += dr;
         col += dc;
         if (col >= W) {
@@ -306,10 +342,13 @@ __global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const
     c.flags = a.flags;
     c.sw = swz<C>(lane);
     c.stage_row = (uint32_t)(lane * C);
-    c.u_row = a.off_u + (uint32_t)(lane * NP * 4);
-    c.v_row = a.off_v + (uint32_t)(lane * NP * 4);
+    constexpr int NB = Geo<N>::NB;
+    c.u_row = a.off_u + (uint32_t)(lane * NB);
+    c.v_row = a.off_v + (uint32_t)(lane * NB);
     c.leaf_row = a.off_leaf + (uint32_t)(lane * NP * 4);
     c.gt_row = a.off_gt + (uint32_t)(lane * NP * 4);
+    c.leaf_g = nullptr;
+    c.gt_g = nullptr;
     {
         uint32_t off = a.off_lvl;
 #pragma unroll
@@ -344,7 +383,17 @@ __global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                              (__attribute__((address_space(3))) void*)(lds + a.off_stage + k * 1024), 16, 0, 0);
         }
-        if (FULL && (a.flags & kGt)) {
+        if constexpr (FULL && R < N) {
+            int64_t grow = row0 + lane;
+            if (grow >= a.B) grow = a.B - 1;
+            c.gt_g = a.gt ? a.gt + grow * N : nullptr;
+            // tail lanes decode a duplicate of the last row; their leaf writes go to a scratch-free
+            // duplicate row only when in range
+            c.leaf_g = (a.leaf && lane < rows) ? a.leaf + (row0 + lane) * N : nullptr;
+            if (a.leaf && lane >= rows) c.flags &= ~kLeaf;
+            else if (a.leaf) c.flags |= kLeaf;
+        }
+        if (FULL && R == N && (a.flags & kGt)) {
             for (int e = lane; e < kWave * N; e += kWave) {
                 const int r = e / N, col = e % N;
                 int64_t grow = row0 + r;
@@ -360,10 +409,10 @@ __global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const
 #pragma unroll
             for (int q = 0; q < C; ++q) {
                 const float4 v = stage_chunk<N>(lds, a.off_stage, c.stage_row, c.sw, q);
-                c.lv[N + 4 * q + 0] = c.scale * v.x;
-                c.lv[N + 4 * q + 1] = c.scale * v.y;
-                c.lv[N + 4 * q + 2] = c.scale * v.z;
-                c.lv[N + 4 * q + 3] = c.scale * v.w;
+                c.lv[N + 4 * q + 0] = rmul(c.scale, v.x);
+                c.lv[N + 4 * q + 1] = rmul(c.scale, v.y);
+                c.lv[N + 4 * q + 2] = rmul(c.scale, v.z);
+                c.lv[N + 4 * q + 3] = rmul(c.scale, v.w);
             }
             node_reg<N, R, PAC, FULL, n, 0>(c, p, a);
         } else {
@@ -387,7 +436,7 @@ __global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const
                         uint32_t bits = w4[w];
                         for (int j = 0; j < kn; ++j) {
                             const int pos = info_lds[k0 + j];  // wave-uniform LDS address: broadcast
-                            const float u = lds_rd(lds, dec_row + 4u * (uint32_t)pos);
+                            const float u = lds_rd8(lds, dec_row + (uint32_t)pos);
                             const float m = (bits & 1u) ? -1.0f : 1.0f;
                             bits >>= 1;
                             e += (u != m) ? 1u : 0u;
@@ -403,9 +452,11 @@ __global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const
 
         // ---- coalesced output stores
         if (a.flags & kMsg)
-            store_rows(lds, PAC ? a.off_v : a.off_u, NP * 4, info_lds, p.K, a.msg, row0, rows, lane);
-        if (FULL && (a.flags & kLeaf)) store_rows(lds, a.off_leaf, NP * 4, nullptr, N, a.leaf, row0, rows, lane);
-        if (FULL && (a.flags & kUhat)) store_rows(lds, a.off_u, NP * 4, nullptr, N, a.uhat, row0, rows, lane);
+            store_rows<true>(lds, PAC ? a.off_v : a.off_u, NB, info_lds, p.K, a.msg, row0, rows, lane);
+        if constexpr (FULL && R == N) {
+            if (a.flags & kLeaf) store_rows<false>(lds, a.off_leaf, NP * 4, nullptr, N, a.leaf, row0, rows, lane);
+        }
+        if (FULL && (a.flags & kUhat)) store_rows<true>(lds, a.off_u, NB, nullptr, N, a.uhat, row0, rows, lane);
     }
 
     if (count) {
@@ -429,25 +480,25 @@ template <int N, int R>
 static Layout make_layout(bool pac, uint32_t flags) {
     Layout L{};
     const uint32_t stage = (uint32_t)(kWave * N * 4);
-    const uint32_t row = (uint32_t)(kWave * (N + 1) * 4);
+    const uint32_t frow = (uint32_t)(kWave * (N + 1) * 4);   // float rows
+    const uint32_t brow = (uint32_t)(kWave * Geo<N>::NB);    // int8 decision rows
     uint32_t off = 0;
     L.off_stage = 0;
     if (R == N) {
-        // the staged tile is fully read into registers before the first decision is written:
-        // the decision rows alias the staging buffer
-        L.off_u = 0;
-        off = align16(stage > row ? stage : row);
+        // the staged tile is fully read into registers before the first leaf: leaf-LLR rows alias it
+        L.off_leaf = 0;
+        off = align16((flags & kLeaf) && frow > stage ? frow : stage);
+        L.off_gt = (flags & kGt) ? off : 0;
+        if (flags & kGt) off = align16(off + frow);
     } else {
         off = align16(stage);
-        L.off_u = off;
-        off = align16(off + row);
+        L.off_leaf = 0;  // leaf LLRs and genie rows go straight to/from HBM
+        L.off_gt = 0;
     }
+    L.off_u = off;
+    off = align16(off + brow);
     L.off_v = pac ? off : 0;
-    if (pac) off = align16(off + row);
-    L.off_leaf = (flags & kLeaf) ? off : 0;
-    if (flags & kLeaf) off = align16(off + row);
-    L.off_gt = (flags & kGt) ? off : 0;
-    if (flags & kGt) off = align16(off + row);
+    if (pac) off = align16(off + brow);
     L.off_lvl = off;
     for (int d = 0; d < 9; ++d)
         if ((1 << d) > R && (1 << d) < N) off += (uint32_t)(kWave * ((1 << d) + 1) * 4);
