@@ -19,6 +19,7 @@ oracle: $(ORACLE)
 
 # per-file extras: the SC kernel never sees NaN (finite LLRs), so fmin needs no canonicalisation
 EXTRA_npd_sc := -fno-honor-nans
+EXTRA_npd_sc_fast := -fno-honor-nans
 
 $(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(CHDR)
 	@mkdir -p $(OBJDIR)
@@ -33,7 +34,7 @@ $(ORACLE): oracle/npd_oracle.c
 
 asm: $(CSRC)
 	@mkdir -p build/asm
-	for f in $(CSRC); do b=$$(basename $$f .hip); $(HIPCC) $(HIPFLAGS) $$( [ $$b = npd_sc ] && echo -fno-honor-nans ) --cuda-device-only -S -o build/asm/$$b.s $$f; done
+	for f in $(CSRC); do b=$$(basename $$f .hip); $(HIPCC) $(HIPFLAGS) $$( case $$b in npd_sc*) echo -fno-honor-nans;; esac ) --cuda-device-only -S -o build/asm/$$b.s $$f; done
 
 clean:
 	rm -rf build $(LIB) $(ORACLE)

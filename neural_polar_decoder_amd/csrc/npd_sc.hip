@@ -16,7 +16,13 @@
 //   min(|a|,|b|) with the xor of the sign bits (identical value, +-0 aside);  g = u*a + b (u in
 //   {-1,0,1}, so the product is exact and fma == mul+add);  leaf = L + prior (polar.py:438, 446);
 //   u = sign(leaf) (polar.py:479).  Partial sums of finished R-blocks are kept as sign/zero bit masks.
+#include <stdlib.h>
+
 #include "npd_common.hpp"
+
+#ifndef NPD_SC_WPE
+#define NPD_SC_WPE 2  // waves per SIMD requested for the register-resident (N <= 64) kernels
+#endif
 
 namespace npd {
 namespace sc {
@@ -174,7 +180,8 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& 
         }
         lds_wr8(c.lds, c.v_row + I, v);
     }
-    lds_wr8(c.lds, c.u_row + I, u);
+    // polar msg-only decoding needs the decisions of information positions only
+    if (PAC || FULL || !frozen) lds_wr8(c.lds, c.u_row + I, u);
     c.beta[I % R] = u;
 }
 
@@ -328,8 +335,9 @@ __device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint3
 }
 
 // ------------------------------------------------------------------------------ kernel
+// N <= 64: every LLR level in VGPRs; ask for <= 256 VGPRs so two waves share each SIMD
 template <int N, int R, bool PAC, bool FULL>
-__global__ __launch_bounds__(64) void sc_decode_kernel(const CodeParams p, const Args a) {
+__global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
     constexpr int C = Geo<N>::C;
@@ -484,8 +492,23 @@ static Layout make_layout(bool pac, uint32_t flags) {
     const uint32_t brow = (uint32_t)(kWave * Geo<N>::NB);    // int8 decision rows
     uint32_t off = 0;
     L.off_stage = 0;
+    const bool full = (flags & (kLeaf | kGt | kUhat)) != 0;
+    if (R == N && !full) {
+        // the staged tile is fully read into registers before the first leaf: decision rows alias it
+        L.off_leaf = 0;
+        L.off_gt = 0;
+        L.off_u = 0;
+        off = align16(stage > brow ? stage : brow);
+        L.off_v = pac ? off : 0;
+        if (pac) off = align16(off + brow);
+        L.off_lvl = off;
+        L.off_info = off;
+        off = align16(off + (uint32_t)(N * 4));
+        L.total = off;
+        return L;
+    }
     if (R == N) {
-        // the staged tile is fully read into registers before the first leaf: leaf-LLR rows alias it
+        // leaf-LLR rows alias the staging buffer (read into registers before the first leaf)
         L.off_leaf = 0;
         off = align16((flags & kLeaf) && frow > stage ? frow : stage);
         L.off_gt = (flags & kGt) ? off : 0;
@@ -562,6 +585,21 @@ static int run(const npd_code* code, Args a, hipStream_t s) {
 
 using namespace npd;
 
+namespace npd {
+bool sc_fast_eligible(const CodeParams& p, const void* y);
+int sc_fast_run(const CodeParams& p, const float* y, float llr_scale, float* msg, unsigned long long* counters,
+                uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s);
+}  // namespace npd
+
+static bool fast_disabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NPD_SC_GENERIC");  // force the generic kernel (testing / A-B)
+        v = (e && *e && *e != '0') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 extern "C" int npd_sc_decode(const npd_code* code, const float* y, float llr_scale, float* leaf_llr, float* msg_hat,
                              float* u_hat, const float* gt, int64_t B, void* stream) {
     NPD_ARG(code != nullptr, "npd_sc_decode: code is NULL");
@@ -577,6 +615,8 @@ extern "C" int npd_sc_decode(const npd_code* code, const float* y, float llr_sca
     a.B = B;
     a.scale = llr_scale;
     a.flags = (leaf_llr ? sc::kLeaf : 0u) | (msg_hat ? sc::kMsg : 0u) | (u_hat ? sc::kUhat : 0u) | (gt ? sc::kGt : 0u);
+    if (!leaf_llr && !u_hat && !gt && B > 0 && !fast_disabled() && sc_fast_eligible(code->p, y))
+        return sc_fast_run(code->p, y, llr_scale, msg_hat, nullptr, 0, 0, B, (hipStream_t)stream);
     return sc::run(code, a, (hipStream_t)stream);
 }
 
@@ -595,5 +635,7 @@ extern "C" int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_
     a.B = B;
     a.scale = llr_scale;
     a.flags = sc::kCount | (msg_hat ? sc::kMsg : 0u);
+    if (B > 0 && !fast_disabled() && sc_fast_eligible(code->p, y))
+        return sc_fast_run(code->p, y, llr_scale, msg_hat, counters, seed, cw_offset, B, (hipStream_t)stream);
     return sc::run(code, a, (hipStream_t)stream);
 }

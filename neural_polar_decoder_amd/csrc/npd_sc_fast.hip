@@ -1,0 +1,279 @@
+// npd_sc_fast.hip -- the hot path: Polar SC min-sum decode for N <= 64, msg_hat + fused counters.
+//
+// Same arithmetic as npd_sc.hip (PolarCode.sc_decode_new, polar.py:465-484; bit-exact), restructured
+// for HBM streaming at one wave per SIMD:
+//   * software pipeline across tiles: while tile t is decoded from VGPRs, the 64 x N fp32 words of
+//     tile t+1 are already in flight as coalesced global_load_dwordx4 into registers (no LDS-DMA, so
+//     the compiler never has to drain them before an LDS access);
+//   * tile t+1 is transposed to one-row-per-lane through an XOR-swizzled LDS image
+//     (ds_write_b128 / ds_read_b128, conflict-free) at the top of its iteration;
+//   * decisions of information positions are written as int8 in SLOT order (rank of the position),
+//     so msg_hat rows are contiguous bytes: the error count compares 4 slots per dword against the
+//     Philox message bits, and msg_hat leaves as coalesced 16-B stores.
+#include "npd_common.hpp"
+
+namespace npd {
+namespace scf {
+
+struct Args {
+    const float* y;
+    float* msg;                      // (B,K) or null
+    unsigned long long* counters;    // {bit errors, block errors} or null
+    uint64_t seed;
+    uint64_t cw_offset;
+    int64_t B;
+    int64_t ntiles;
+    float scale;
+    uint32_t count;
+};
+
+__device__ __forceinline__ float rmul(float a, float b) {
+    float r = a * b;
+    asm("" : "+v"(r));  // keep fl32(scale*y) rounded (no fma contraction), as polar.py:468
+    return r;
+}
+
+__device__ __forceinline__ float f_minsum(float a, float b) {
+    const float m = __builtin_fminf(__builtin_fabsf(a), __builtin_fabsf(b));
+    return bitsf(fbits(m) | ((fbits(a) ^ fbits(b)) & 0x80000000u));
+}
+
+__device__ __forceinline__ float sgn_bits(float x) {
+    const float s = bitsf((fbits(x) & 0x80000000u) | 0x3f800000u);
+    return (x == 0.0f) ? 0.0f : s;
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+struct Lane {
+    float lv[2 * N];   // level d at lv[2^d .. 2^(d+1)); input level at lv[N .. 2N)
+    float beta[N];
+    char* lds;
+    uint32_t u_row;    // byte address of this lane's decision row (slot order)
+};
+
+template <int N, int I>
+__device__ __forceinline__ void leaf(Lane<N>& c, const CodeParams& p, float L) {
+    const bool frozen = (p.frozen[I >> 5] >> (I & 31)) & 1u;
+    const float lf = L + (frozen ? p.infty : 0.0f);  // polar.py:438/446
+    const float u = sgn_bits(lf);                     // polar.py:479
+    if (!frozen) *reinterpret_cast<int8_t*>(c.lds + c.u_row + p.rank[I]) = (int8_t)(int)u;
+    c.beta[I] = u;
+}
+
+template <int N, int D, int S0>
+__device__ __forceinline__ void node(Lane<N>& c, const CodeParams& p) {
+    if constexpr (D == 0) {
+        leaf<N, S0>(c, p, c.lv[1]);
+    } else {
+        constexpr int h = 1 << (D - 1);
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
+        node<N, D - 1, S0>(c, p);
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[S0 + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+        node<N, D - 1, S0 + h>(c, p);
+        if constexpr ((1 << D) < N) {
+#pragma unroll
+            for (int j = 0; j < h; ++j) c.beta[S0 + j] = c.beta[S0 + j] * c.beta[S0 + h + j];
+        }
+    }
+}
+
+template <int N>
+constexpr int log2c() {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    return n;
+}
+
+template <int C>
+__device__ __forceinline__ int swz(int r) {
+    if constexpr (C >= 16) return r & 15;
+    else return (r / (16 / C)) % C;
+}
+
+// number of nonzero bytes in x
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t x) {
+    const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+    return (uint32_t)__builtin_popcount(t & 0x80808080u);
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void sc_fast_kernel(const CodeParams p, const Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int n = log2c<N>();
+    constexpr int C = N / 4;                 // 16-B chunks per row (and per lane per tile)
+    constexpr int NB = 4 * ((N / 4) | 1);    // decision-row stride in bytes (odd dword count)
+    constexpr uint32_t kStage = 0;
+    constexpr uint32_t kU = kWave * N * 4;
+    const int lane = threadIdx.x;
+    const int K = p.K;
+
+    Lane<N> c;
+    c.lds = lds;
+    c.u_row = kU + (uint32_t)(lane * NB);
+    const int sw = swz<C>(lane);
+
+    uint32_t err_bits = 0, err_blocks = 0;
+    const f4* y4 = reinterpret_cast<const f4*>(a.y);
+    const int64_t last4 = a.B * C - 1;  // last valid float4 of y
+
+    // prefetch registers: chunk q of tile t for this lane = float4 index t*64*C + lane + 64*q
+    f4 nx[C];
+    int64_t t = blockIdx.x;
+    if (t < a.ntiles) {
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            int64_t gi = t * (int64_t)(kWave * C) + lane + kWave * q;
+            nx[q] = y4[gi < last4 ? gi : last4];
+        }
+    }
+    for (; t < a.ntiles; t += gridDim.x) {
+        const int64_t row0 = t * kWave;
+        const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
+        // ---- transpose the tile through LDS: chunk (lane + 64q) -> row r = (lane + 64q)/C, col chunk
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const int pch = lane + kWave * q;
+            const int r = pch / C, cc = pch % C;
+            *reinterpret_cast<f4*>(lds + kStage + 16u * (uint32_t)(r * C + (cc ^ swz<C>(r)))) = nx[q];
+        }
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
+            c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
+            c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
+            c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
+            c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+        }
+        // ---- prefetch the next tile (lands while this one is decoded)
+        const int64_t tn = t + gridDim.x;
+        if (tn < a.ntiles) {
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                int64_t gi = tn * (int64_t)(kWave * C) + lane + kWave * q;
+                nx[q] = y4[gi < last4 ? gi : last4];
+            }
+        }
+        // ---- decode
+        node<N, n, 0>(c, p);
+
+        // ---- error count: 4 slots per dword vs the Philox message bits (errors_ber/bler semantics)
+        if (a.count) {
+            const uint64_t cw = a.cw_offset + (uint64_t)(row0 + lane);
+            const u32x4 o = philox_block(a.seed, kStreamMsg, cw, 0u);
+            const uint32_t mw[4] = {o.x, o.y, o.z, o.w};
+            uint32_t e = 0;
+#pragma unroll
+            for (int w = 0; w < N / 4; ++w) {
+                if (4 * w < K) {
+                    const uint32_t dec = *reinterpret_cast<const uint32_t*>(lds + c.u_row + 4 * w);
+                    const uint32_t nib = (mw[(4 * w) >> 5] >> ((4 * w) & 31)) & 0xFu;
+                    const uint32_t x = (nib * 0x00204081u) & 0x01010101u;  // bit i -> byte i
+                    const uint32_t expect = 0x01010101u | (x * 0xFEu);       // +1 -> 0x01, -1 -> 0xFF
+                    const int valid = K - 4 * w;                               // slots in this dword
+                    const uint32_t vmask = valid >= 4 ? 0xFFFFFFFFu : ((1u << (8 * valid)) - 1u);
+                    e += nz_bytes((dec ^ expect) & vmask);
+                }
+            }
+            if (lane < rows) {
+                err_bits += e;
+                err_blocks += e ? 1u : 0u;
+            }
+        }
+
+        // ---- msg_hat: the tile's rows*K floats are contiguous in HBM
+        if (a.msg) {
+            float* dst = a.msg + row0 * (int64_t)K;
+            const int total = rows * K;
+            if ((K & 3) == 0) {
+                int f = 4 * lane;
+                int r = f / K, col = f % K;
+                const int dr = 256 / K, dc = 256 % K;
+                for (; f < total; f += 256) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(lds + kU + (uint32_t)(r * NB + col));
+                    f4 o;
+                    o.x = (float)(int8_t)(w & 0xFFu);
+                    o.y = (float)(int8_t)((w >> 8) & 0xFFu);
+                    o.z = (float)(int8_t)((w >> 16) & 0xFFu);
+                    o.w = (float)(int8_t)(w >> 24);
+                    *reinterpret_cast<f4*>(dst + f) = o;
+                    r += dr;
+                    col += dc;
+                    if (col >= K) {
+                        col -= K;
+                        ++r;
+                    }
+                }
+            } else {
+                int r = lane / K, col = lane % K;
+                const int dr = kWave / K, dc = kWave % K;
+                for (int f = lane; f < total; f += kWave) {
+                    dst[f] = (float)*reinterpret_cast<const int8_t*>(lds + kU + (uint32_t)(r * NB + col));
+                    r += dr;
+                    col += dc;
+                    if (col >= K) {
+                        col -= K;
+                        ++r;
+                    }
+                }
+            }
+        }
+    }
+
+    if (a.count) {
+        const uint32_t eb = wave_sum_u32(err_bits);
+        const uint32_t bl = wave_sum_u32(err_blocks);
+        if (lane == 0) {
+            atomicAdd(a.counters + 0, (unsigned long long)eb);
+            atomicAdd(a.counters + 1, (unsigned long long)bl);
+        }
+    }
+}
+
+template <int N>
+static int launch(const CodeParams& p, Args a, hipStream_t s) {
+    constexpr int NB = 4 * ((N / 4) | 1);
+    const size_t lds = (size_t)kWave * N * 4 + (size_t)kWave * NB;
+    a.ntiles = (a.B + kWave - 1) / kWave;
+    auto kern = sc_fast_kernel<N>;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, s, p, a);
+    return launch_check("sc_fast_kernel launch");
+}
+
+}  // namespace scf
+
+// eligible: Polar, 8 <= N <= 64, K <= 128 (one Philox block of message bits), y 16-B aligned
+bool sc_fast_eligible(const CodeParams& p, const void* y) {
+    return !p.pac && p.N >= 8 && p.N <= 64 && p.K <= 128 && (((uintptr_t)y) & 15) == 0;
+}
+
+int sc_fast_run(const CodeParams& p, const float* y, float llr_scale, float* msg, unsigned long long* counters,
+                uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s) {
+    scf::Args a{};
+    a.y = y;
+    a.msg = msg;
+    a.counters = counters;
+    a.seed = seed;
+    a.cw_offset = cw_offset;
+    a.B = B;
+    a.scale = llr_scale;
+    a.count = counters ? 1u : 0u;
+    switch (p.N) {
+        case 8: return scf::launch<8>(p, a, s);
+        case 16: return scf::launch<16>(p, a, s);
+        case 32: return scf::launch<32>(p, a, s);
+        case 64: return scf::launch<64>(p, a, s);
+        default: return fail(NPD_EINVAL, "sc_fast: unsupported N");
+    }
+}
+
+}  // namespace npd
