@@ -100,6 +100,32 @@ def cpu_baseline(ys_host, snrs, info, budget_s):
             "reference_measured_8core": 4.67e3}
 
 
+def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
+    """Secondary line (configs[2]): CRISP GRU hidden 64, 2 layers, Polar(64,32), fused decode kernel.
+    Seeded random weights (no trained checkpoint ships with the reference)."""
+    from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
+    torch.manual_seed(0)
+    net = RNN_Model("GRU", N_CODE + 2, 64, 1, 2, N_CODE, 0, 0).to(dev)
+    dec = RNN_decoder("y_input", N_CODE, code.info_positions, onehot=True)
+    yb = y[:batch].contiguous()
+    dec.decode(net, False, yb)  # warm (weights packed once)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        dec.decode(net, False, yb)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    F, N = 64, N_CODE
+    flop_cw = 2 * 3 * F * N + N * (2 * 3 * F * F + 2 * 2 * 3 * F * F + 2 * F)  # SURVEY.md 8(d): 4.751 MFLOP
+    tflops = flop_cw * batch / (ms / 1e3) / 1e12
+    return {"value": batch / (ms / 1e3), "unit": "codewords/s", "batch": batch, "avg_launch_ms": ms,
+            "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "algorithmic_flop_per_cw": flop_cw,
+            "achieved_tflops": tflops, "peak_tflops_fp32": 157.3, "frac": tflops / 157.3,
+            "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input"}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -186,6 +212,8 @@ def main():
         "bler": {str(s): bler[s] for s in snrs},
         "ber_match": bool(ber_match),
     }
+    if not args.no_gru:
+        out["crisp_gru"] = gru_measure(code, dev, ys[2], snrs[2])
     if not args.no_cpu_baseline:
         ys_host = [y[: 1 << 18].cpu().numpy() for y in ys]
         out["cpu_baseline"] = cpu_baseline(ys_host, snrs, code.info_positions, args.cpu_seconds)

@@ -1,0 +1,420 @@
+// npd_gru.hip -- CRISP GRU autoregressive decoder (RNN_decoder.decode, y_input, test branch).
+//
+// Reference: rnn_all.py:294-398 (RNN_Model: nn.GRU(N+2, F, layers) + Linear(F, 1)), rnn_all.py:532-547
+// (per-bit loop: x_i = [y, onehot(prev)], one GRU step, d_i = sign(out) on information positions),
+// get_onehot rnn_all.py:258-260, PyTorch GRUCell (r, z, n gate order; h' = (h - n) * z + n).
+//
+// MI355X design: the per-step matvecs of all codewords of a wave form GEMMs
+//   gates^T (3F x 32 codewords) = W (3F x F) . h^T (F x 32)
+// computed with v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains).  Gate rows are the MFMA rows and
+// codewords the columns, so a 32x32 accumulator tile of h' is, register for register, the B operand
+// of the next step's MFMAs (no transpose, no LDS round trip for the state); the weight matrices are
+// permuted once on the host into the matching A-operand order and live in LDS for the whole launch
+// (one 256-thread workgroup per CU, four waves, 32 codewords per wave).  The y part of the input
+// projection, W_ih0[:, :N] y, is constant over the N steps and computed once per codeword (P); the
+// one-hot / previous-decision column and all biases are folded into one extra MFMA k-step whose B
+// operand is [1, x_i].
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "npd_common.hpp"
+
+struct npd_gru {
+    int N, F, layers, onehot, precision, device;
+    float b_lin;
+    float* img;   // LDS image (device)
+    float* wy;    // y-projection A operands (device)
+    int64_t img_floats;
+};
+
+namespace npd {
+namespace gru {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+template <int F, int L>
+struct Geo {
+    static constexpr int TT = 3 * F / 32;  // 32-row tiles of the 3F gate rows
+    static constexpr int HT = F / 32;      // 32-row tiles of the hidden state
+    static constexpr int KS = F / 2;       // k-steps (2 hidden units each) per matvec
+    static constexpr int KG = KS / 4;      // groups of 4 k-steps (one ds_read_b128)
+    static constexpr int NG = (L == 2) ? 3 : 1;     // weight images: L0 hh, L1 ih, L1 hh
+    static constexpr int G_SIZE = TT * KG * 64 * 4;  // floats per image
+    static constexpr int OFF_X = NG * G_SIZE;        // extra k-step A operands [g][t][64]
+    static constexpr int OFF_IN = OFF_X + NG * TT * 64;  // layer-0 n-gate input extra [HT][64]
+    static constexpr int OFF_WL = OFF_IN + HT * 64;      // linear weights [half][HT][16]
+    static constexpr int TOTAL = OFF_WL + 2 * HT * 16;
+};
+
+// hidden unit fed by lane half `kk` at k-step s (accumulator row map of the 32x32 MFMA tile)
+__host__ __device__ inline int hid_of(int s, int kk) {
+    const int i = s & 15;
+    return 32 * (s >> 4) + (i & 3) + 8 * (i >> 2) + 4 * kk;
+}
+
+struct Args {
+    const float* img;
+    const f4* wy;
+    const float* y;
+    const float* gt;
+    float* decoded;
+    float* logits;
+    int64_t B;
+    int N;
+    int rev;
+    int onehot;
+    float b_lin;
+    uint32_t info[kMaxWords];
+};
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// acc[0..NT) += W_g[tiles t0..t0+NT) . h  over all KS k-steps.  Weight groups (4 k-steps, one
+// ds_read_b128 per tile) are read one group ahead of the MFMAs that consume them; the empty asm with a
+// memory clobber bounds that look-ahead so the weights of a whole matvec are never hoisted into VGPRs.
+template <int TT, int KG, int NT, int HT>
+__device__ __forceinline__ void gemm_chain(const f4* __restrict__ smem4, int g, int t0, int lane, f16v (&acc)[NT],
+                                           const f16v (&h)[HT]) {
+    f4 wc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wc[t] = smem4[((g * TT + t0 + t) * KG + 0) * 64 + lane];
+#pragma unroll
+    for (int s4 = 0; s4 < KG; ++s4) {
+        f4 wn[NT];
+        if (s4 + 1 < KG) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) wn[t] = smem4[((g * TT + t0 + t) * KG + s4 + 1) * 64 + lane];
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int s = 4 * s4 + e;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma(wc[t][e], h[s >> 4][s & 15], acc[t]);
+        }
+        if (s4 + 1 < KG) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) wc[t] = wn[t];
+        }
+    }
+}
+
+// PyTorch GRUCell update on one 32x32 tile pair: h = (h - n) * z + n,
+// r = sigmoid(a_r), z = sigmoid(a_z), n = tanh(a_in + r * a_hn)
+__device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float r = sigmoidf_(ar[i]);
+        const float z = sigmoidf_(az[i]);
+        const float nn = tanhf(ain[i] + ahn[i] * r);
+        h[i] = (h[i] - nn) * z + nn;
+    }
+}
+
+template <int F, int L>
+__global__ __launch_bounds__(256) void gru_decode_kernel(const Args a) {
+    using G = Geo<F, L>;
+    constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
+    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
+    const float* smem = reinterpret_cast<const float*>(smem4);
+    {
+        const f4* src = reinterpret_cast<const f4*>(a.img);
+        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int half = lane >> 5;
+    const int col = lane & 31;
+    const int N = a.N;
+    const int64_t ntiles = (a.B + 31) / 32;
+    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+        const int64_t cw = tile * 32 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+
+        // ---- P = W_ih0[:, :N] . y  (k-step s pairs y[s] (half 0) with y[s + N/2] (half 1))
+        f16v P[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) P[t] = zero;
+        {
+            const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
+            const int ng = N / 8;
+            for (int s4 = 0; s4 < ng; ++s4) {
+                const f4 yv = yr[s4];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const f4 w = a.wy[(t * ng + s4) * 64 + lane];
+                    P[t] = mfma(w.x, yv.x, P[t]);
+                    P[t] = mfma(w.y, yv.y, P[t]);
+                    P[t] = mfma(w.z, yv.z, P[t]);
+                    P[t] = mfma(w.w, yv.w, P[t]);
+                }
+            }
+        }
+
+        f16v h0[HT], h1[HT];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+            h0[t] = zero;
+            h1[t] = zero;
+        }
+        float xb = 1.0f;  // x_i: onehot index of the previous decision (or its sign); step 0: prev = +1
+        const float one_or_zero = half ? 0.0f : 1.0f;
+
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            const float xbe = half ? xb : 1.0f;  // extra k-step B operand: [1, x_i]
+            // ================= layer 0: acc = P + W_hh0 h0 + consts + x_i column
+            {
+                f16v acc[TT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
+#pragma unroll
+                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
+                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                }
+            }
+            if constexpr (L == 2) {
+                // ================= layer 1: acc1 = W_ih1 h0' (+ W_hh1 h1 on r,z rows); ahn = W_hh1_n h1
+                f16v acc1[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
+                f16v arz[2 * HT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
+                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 2, 0, lane, arz, h1);
+                f16v ahn[HT];
+#pragma unroll
+                for (int j = 0; j < HT; ++j) ahn[j] = zero;
+                gemm_chain<TT, KG, HT, HT>(smem4, 2, 2 * HT, lane, ahn, h1);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
+                    gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
+                }
+            }
+            // ================= output: Linear(F, 1) on the top layer
+            float part = 0.0f;
+#pragma unroll
+            for (int t = 0; t < HT; ++t) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float wl = smem[G::OFF_WL + (half * HT + t) * 16 + i];
+                    part += wl * (L == 2 ? h1[t][i] : h0[t][i]);
+                }
+            }
+            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+            float d;
+            if (info) {
+                d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+            } else {
+                d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+            }
+            if (half == 0 && valid) {
+                a.decoded[cw * N + jj] = d;
+                if (a.logits) a.logits[cw * N + ii] = out;
+            }
+            // next input: onehot(sign(d)) -> index (0.5 + 0.5*s).long() (rnn_all.py:258-260); else sign(d)
+            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------- host image
+template <int F, int L>
+static void build_image(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
+                        float& b_lin) {
+    using G = Geo<F, L>;
+    constexpr int TT = G::TT, HT = G::HT, KG = G::KG, KS = G::KS;
+    const int Din = N + (onehot ? 2 : 1);
+    // unpack
+    const float* p = W;
+    const float* wih[2];
+    const float* whh[2];
+    const float* bih[2];
+    const float* bhh[2];
+    for (int l = 0; l < L; ++l) {
+        const int din = l == 0 ? Din : F;
+        wih[l] = p; p += (size_t)3 * F * din;
+        whh[l] = p; p += (size_t)3 * F * F;
+        bih[l] = p; p += 3 * F;
+        bhh[l] = p; p += 3 * F;
+    }
+    const float* wlin = p;
+    b_lin = p[F];
+    img.assign(G::TOTAL, 0.0f);
+    // main k-steps of the three images
+    const float* mats[3] = {whh[0], L == 2 ? wih[1] : nullptr, L == 2 ? whh[1] : nullptr};
+    for (int g = 0; g < G::NG; ++g)
+        for (int t = 0; t < TT; ++t)
+            for (int s = 0; s < KS; ++s)
+                for (int l = 0; l < 64; ++l) {
+                    const int row = 32 * t + (l & 31);
+                    const int h = hid_of(s, l >> 5);
+                    img[((size_t)(g * TT + t) * KG + s / 4) * 256 + l * 4 + (s & 3)] = mats[g][(size_t)row * F + h];
+                }
+    // extra k-step A operands: column 0 pairs with B = 1, column 1 with B = x_i (layer 0) / 0 (layer 1)
+    for (int t = 0; t < TT; ++t)
+        for (int l = 0; l < 64; ++l) {
+            const int row = 32 * t + (l & 31);
+            const int kk = l >> 5;
+            const bool rz = row < 2 * F;
+            // layer 0, hidden-side image: r,z rows carry every input-side constant too
+            float v0;
+            if (kk == 0) {
+                v0 = rz ? bih[0][row] + bhh[0][row] + (onehot ? wih[0][(size_t)row * Din + N] : 0.0f) : bhh[0][row];
+            } else {
+                v0 = rz ? (onehot ? wih[0][(size_t)row * Din + N + 1] - wih[0][(size_t)row * Din + N]
+                                  : wih[0][(size_t)row * Din + N])
+                        : 0.0f;
+            }
+            img[G::OFF_X + (0 * TT + t) * 64 + l] = v0;
+            if (L == 2) {
+                img[G::OFF_X + (1 * TT + t) * 64 + l] = kk == 0 ? (rz ? bih[1][row] + bhh[1][row] : bih[1][row]) : 0.0f;
+                img[G::OFF_X + (2 * TT + t) * 64 + l] = kk == 0 ? (rz ? 0.0f : bhh[1][row]) : 0.0f;
+            }
+        }
+    for (int j = 0; j < HT; ++j)
+        for (int l = 0; l < 64; ++l) {
+            const int row = 2 * F + 32 * j + (l & 31);
+            const int kk = l >> 5;
+            float v;
+            if (kk == 0) v = bih[0][row] + (onehot ? wih[0][(size_t)row * Din + N] : 0.0f);
+            else v = onehot ? wih[0][(size_t)row * Din + N + 1] - wih[0][(size_t)row * Din + N] : wih[0][(size_t)row * Din + N];
+            img[G::OFF_IN + j * 64 + l] = v;
+        }
+    for (int hf = 0; hf < 2; ++hf)
+        for (int t = 0; t < HT; ++t)
+            for (int i = 0; i < 16; ++i) img[G::OFF_WL + (hf * HT + t) * 16 + i] = wlin[32 * t + (i & 3) + 8 * (i >> 2) + 4 * hf];
+    // y projection: k-step s pairs y[s] (lanes 0-31) with y[s + N/2] (lanes 32-63)
+    const int ng = N / 8;
+    wy.assign((size_t)TT * ng * 256, 0.0f);
+    for (int t = 0; t < TT; ++t)
+        for (int s = 0; s < N / 2; ++s)
+            for (int l = 0; l < 64; ++l) {
+                const int row = 32 * t + (l & 31);
+                const int k = s + (l >> 5) * (N / 2);
+                wy[((size_t)t * ng + s / 4) * 256 + l * 4 + (s & 3)] = wih[0][(size_t)row * Din + k];
+            }
+}
+
+template <int F, int L>
+static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
+    using G = Geo<F, L>;
+    auto kern = gru_decode_kernel<F, L>;
+    const size_t lds = (size_t)G::TOTAL * 4;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    const int64_t tiles = (a.B + 31) / 32;
+    const int64_t wgs = (tiles + 3) / 4;
+    const int grid = grid_for(wgs, 1, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+    (void)g;
+    return launch_check("gru_decode_kernel launch");
+}
+
+}  // namespace gru
+}  // namespace npd
+
+using namespace npd;
+
+extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights,
+                              int precision, npd_gru** out) {
+    NPD_ARG(out != nullptr, "npd_gru_create: out is NULL");
+    *out = nullptr;
+    NPD_ARG(weights != nullptr, "npd_gru_create: weights is NULL");
+    NPD_ARG(N >= 8 && N <= kMaxN && N % 8 == 0, "npd_gru_create: N must be a multiple of 8 in [8, 256]");
+    NPD_ARG(F == 32 || F == 64, "npd_gru_create: hidden size F must be 32 or 64 in this build");
+    NPD_ARG(layers == 1 || layers == 2, "npd_gru_create: 1 or 2 GRU layers supported");
+    NPD_ARG(precision == 0, "npd_gru_create: only fp32 (precision 0) is built");
+    const int Din = N + (onehot ? 2 : 1);
+    int64_t expect = (int64_t)3 * F * Din + (int64_t)3 * F * F + 6 * F;
+    if (layers == 2) expect += (int64_t)6 * F * F + 6 * F;
+    expect += F + 1;
+    NPD_ARG(n_weights == expect, "npd_gru_create: weight count does not match (N, F, layers, onehot)");
+    std::vector<float> img, wy;
+    float b_lin = 0.0f;
+    if (F == 64 && layers == 2) gru::build_image<64, 2>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 64) gru::build_image<64, 1>(weights, N, onehot, img, wy, b_lin);
+    else if (layers == 2) gru::build_image<32, 2>(weights, N, onehot, img, wy, b_lin);
+    else gru::build_image<32, 1>(weights, N, onehot, img, wy, b_lin);
+    npd_gru* g = new (std::nothrow) npd_gru;
+    if (!g) return fail(NPD_ENOMEM, "npd_gru_create: out of memory");
+    memset(g, 0, sizeof(*g));
+    g->N = N; g->F = F; g->layers = layers; g->onehot = onehot; g->precision = precision; g->b_lin = b_lin;
+    g->img_floats = (int64_t)img.size();
+    hipError_t e = hipGetDevice(&g->device);
+    if (e == hipSuccess) e = hipMalloc(&g->img, img.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&g->wy, wy.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(g->img, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(g->wy, wy.data(), wy.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (g->img) (void)hipFree(g->img);
+        if (g->wy) (void)hipFree(g->wy);
+        delete g;
+        return hip_fail(e, "npd_gru_create");
+    }
+    *out = g;
+    return NPD_OK;
+}
+
+extern "C" int npd_gru_destroy(npd_gru* g) {
+    if (!g) return NPD_OK;
+    if (g->img) (void)hipFree(g->img);
+    if (g->wy) (void)hipFree(g->wy);
+    delete g;
+    return NPD_OK;
+}
+
+extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* is_info, int reverse, const float* gt,
+                              float* decoded, float* logits, int64_t B, void* stream) {
+    NPD_ARG(g != nullptr, "npd_gru_decode: gru is NULL");
+    NPD_ARG(B >= 0, "npd_gru_decode: B < 0");
+    if (B == 0) return NPD_OK;
+    NPD_ARG(y != nullptr && decoded != nullptr && is_info != nullptr, "npd_gru_decode: null pointer");
+    NPD_ARG(((uintptr_t)y & 15) == 0, "npd_gru_decode: y must be 16-byte aligned");
+    gru::Args a{};
+    a.img = g->img;
+    a.wy = reinterpret_cast<const gru::f4*>(g->wy);
+    a.y = y;
+    a.gt = gt;
+    a.decoded = decoded;
+    a.logits = logits;
+    a.B = B;
+    a.N = g->N;
+    a.rev = reverse ? 1 : 0;
+    a.onehot = g->onehot;
+    a.b_lin = g->b_lin;
+    for (int w = 0; w < kMaxWords; ++w) a.info[w] = 0;
+    for (int i = 0; i < g->N; ++i)
+        if (is_info[i]) a.info[i >> 5] |= 1u << (i & 31);
+    hipStream_t s = (hipStream_t)stream;
+    if (g->F == 64 && g->layers == 2) return gru::launch<64, 2>(g, a, s);
+    if (g->F == 64) return gru::launch<64, 1>(g, a, s);
+    if (g->layers == 2) return gru::launch<32, 2>(g, a, s);
+    return gru::launch<32, 1>(g, a, s);
+}

@@ -2,14 +2,6 @@
 #include "npd_common.hpp"
 
 extern "C" {
-int npd_gru_create(int, int, int, int, const float*, int64_t, int, npd_gru** out) {
-    if (out) *out = nullptr;
-    return npd::fail(NPD_ENOTSUP, "npd_gru_create: not built yet");
-}
-int npd_gru_destroy(npd_gru*) { return NPD_OK; }
-int npd_gru_decode(const npd_gru*, const float*, const uint8_t*, int, const float*, float*, float*, int64_t, void*) {
-    return npd::fail(NPD_ENOTSUP, "npd_gru_decode: not built yet");
-}
 int npd_conv_create(int, int, const float*, int64_t, int, npd_conv** out) {
     if (out) *out = nullptr;
     return npd::fail(NPD_ENOTSUP, "npd_conv_create: not built yet");

@@ -1,0 +1,151 @@
+"""CRISP GRU decoder -- drop-in for rnn_all.RNN_Model / RNN_decoder (rnn_all.py:294-561).
+
+``RNN_Model`` keeps the reference's constructor and parameter names (``rnn.weight_ih_l0`` ...,
+``linear.weight``) so reference state dicts / checkpoints load unchanged; it is the weight container
+(its ``forward`` is the reference's single-step training API, plain PyTorch).  The decode hot path,
+``RNN_decoder.decode(net, False, y, ...)`` (rnn_all.py:532-547), runs the whole N-step
+autoregressive loop in one fused HIP kernel (npd_gru_decode; fp32 MFMA).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+class RNN_Model(nn.Module):
+    """Same parameters as the reference (rnn_all.py:294-385).  Only the configuration the CRISP
+    y_input eval uses is accepted by the fused decoder: GRU, output_size 1, y_depth 0,
+    out_linear_depth 1, unidirectional, no layernorm."""
+
+    def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
+                 y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
+                 bidirectional=False, use_layernorm=False):
+        super().__init__()
+        assert rnn_type in ["GRU", "LSTM"]
+        self.rnn_type = rnn_type
+        self.input_size = input_size
+        self.feature_size = feature_size
+        self.output_size = output_size
+        self.num_rnn_layers = num_rnn_layers
+        self.bidirectional = bidirectional
+        self.y_size = y_size
+        self.y_hidden_size = y_hidden_size
+        self.y_depth = y_depth
+        self.out_linear_depth = out_linear_depth
+        self.activation = activation
+        self.skip = skip
+        self.rnn = getattr(nn, rnn_type)(input_size, feature_size, num_rnn_layers, bidirectional=bidirectional,
+                                         batch_first=True)
+        self.drop = nn.Dropout(dropout)
+        self.layernorm = nn.LayerNorm(feature_size) if use_layernorm else nn.Identity()
+        if out_linear_depth == 1:
+            self.linear = nn.Linear((int(bidirectional) + 1) * feature_size, output_size)
+        else:
+            layers = [nn.Linear((int(bidirectional) + 1) * feature_size, y_hidden_size)]
+            for _ in range(1, out_linear_depth - 1):
+                layers += [nn.SELU(), nn.Linear(y_hidden_size, y_hidden_size)]
+            layers += [nn.SELU(), nn.Linear(y_hidden_size, output_size)]
+            self.linear = nn.Sequential(*layers)
+
+    def forward(self, input, hidden, Fy=None):
+        """Single recurrent step (rnn_all.py:387-398) -- the training-time API."""
+        out, hidden = self.rnn(input, hidden)
+        out = self.layernorm(self.drop(out))
+        decoded = self.linear(out if Fy is None else torch.cat([Fy, out], -1))
+        return decoded.view(-1, self.output_size), hidden
+
+    def fused_supported(self) -> bool:
+        return (self.rnn_type == "GRU" and self.output_size == 1 and self.y_depth == 0 and self.out_linear_depth == 1
+                and not self.bidirectional and isinstance(self.layernorm, nn.Identity)
+                and self.feature_size in (32, 64) and self.num_rnn_layers in (1, 2))
+
+
+def pack_gru_weights(net: nn.Module, layers: int) -> np.ndarray:
+    """Flatten the state dict in the order of include/npd.h npd_gru_create."""
+    sd = net.state_dict()
+    parts = []
+    for l in range(layers):
+        for nm in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+            parts.append(sd[f"rnn.{nm}_l{l}"].detach().float().cpu().numpy().ravel())
+    parts.append(sd["linear.weight"].detach().float().cpu().numpy().ravel())
+    parts.append(sd["linear.bias"].detach().float().cpu().numpy().ravel())
+    return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
+
+
+class _GruHandle:
+    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0):
+        L = _lib.load()
+        out = ctypes.c_void_p()
+        _lib.check(L.npd_gru_create(int(N), int(F), int(layers), 1 if onehot else 0, W.ctypes.data_as(ctypes.c_void_p),
+                                    int(W.size), int(precision), ctypes.byref(out)), "npd_gru_create")
+        self.h = out
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.load().npd_gru_destroy(self.h)
+        except Exception:
+            pass
+
+
+class RNN_decoder:
+    """rnn_all.RNN_decoder (rnn_all.py:400-561): eval (``train=False``) decoding for decoding_type
+    'y_input' runs fused on the GPU."""
+
+    def __init__(self, decoding_type, N, info_inds, onehot=False, reverse_order=False):
+        self.decoding_type = decoding_type
+        self.N = N
+        self.info_inds = info_inds
+        self.onehot = onehot
+        self.reverse_order = reverse_order
+        self._cache = {}
+
+    def _handle(self, net: RNN_Model, device):
+        # re-pack when the weights change (parameter versions) or the device differs
+        key = (id(net), str(device), tuple(p._version for p in net.parameters()),
+               tuple(p.data_ptr() for p in net.parameters()))
+        h = self._cache.get(key)
+        if h is None:
+            self._cache.clear()
+            W = pack_gru_weights(net, net.num_rnn_layers)
+            with torch.cuda.device(device):
+                h = _GruHandle(self.N, net.feature_size, net.num_rnn_layers, self.onehot, W)
+            self._cache[key] = h
+        return h
+
+    def decode(self, net, train, y, gt=None, teacher_forcing_ratio=0., loss_inds=None, return_logits=False):
+        if train:
+            raise _lib.NpdError("RNN_decoder.decode(train=True) is the training path (out of scope for the fused "
+                                "decoder); use the reference's PyTorch loop for training")
+        if self.decoding_type != "y_input":
+            raise _lib.NpdError(f"fused decode supports decoding_type 'y_input', got {self.decoding_type!r}")
+        if not (hasattr(net, "fused_supported") and net.fused_supported()):
+            raise _lib.NpdError("network configuration not supported by the fused GRU decoder")
+        if net.input_size != self.N + 1 + int(self.onehot):
+            raise ValueError("net.input_size must be N + 1 + onehot")
+        _lib.require_gpu(y, "y")
+        y = _lib.f32c(y)
+        B = y.shape[0]
+        if loss_inds is None:
+            loss_inds = self.info_inds
+        is_info = np.zeros(self.N, np.uint8)
+        is_info[np.asarray(loss_inds, np.int64)] = 1
+        h = self._handle(net, y.device)
+        dec = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
+        logits = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_logits else None
+        g = None if gt is None else _lib.f32c(gt.to(y.device))
+        _lib.check(_lib.load().npd_gru_decode(h.h, _lib.ptr(y), is_info.ctypes.data_as(ctypes.c_void_p),
+                                              1 if self.reverse_order else 0, _lib.ptr(g), _lib.ptr(dec),
+                                              _lib.ptr(logits), B, _lib.stream_of(y.device)), "npd_gru_decode")
+        return (dec, logits) if return_logits else dec
+
+
+def get_onehot(actions):
+    """rnn_all.py:258-260."""
+    inds = (0.5 + 0.5 * actions).long()
+    return torch.eye(2, device=inds.device)[inds].reshape(actions.shape[0], -1)

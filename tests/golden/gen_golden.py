@@ -198,7 +198,7 @@ def gen_errors():
 def gen_gru():
     cases = [("gru_polar_64_32", "Polar", 64, 32, 64, True, False, 512),
              ("gru_pac_128_64", "PAC", 128, 64, 64, True, False, 128),
-             ("gru_polar_16_8_noonehot_rev", "Polar", 16, 8, 16, False, True, 256)]
+             ("gru_polar_16_8_noonehot_rev", "Polar", 16, 8, 32, False, True, 256)]
     for name, ctype, N, K, F, onehot, rev, B in cases:
         torch.manual_seed(2024 + N)
         if ctype == "Polar":
