@@ -230,3 +230,31 @@ def test_ber_curve_matches_reference_anchors():
         # bit errors cluster within blocks: bound with the block-level variance of errors per block
         se_ber = np.sqrt((1 / 1e5 + 1 / B)) * np.sqrt(bler_ref) * (ber_ref / max(bler_ref, 1e-9)) * 2.5
         assert abs(ber - ber_ref) < 4 * se_ber + 1e-12, (snr, ber, ber_ref)
+
+
+def test_montecarlo_driver_shard_invariance():
+    """SCMonteCarlo: simulated 3-rank shards (summed) == one rank, exactly (Philox keyed by codeword)."""
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import SCMonteCarlo
+    code = reference_polar_code(64, 32)
+    snrs = [0.0, 1.0, 2.0]
+    one = SCMonteCarlo(code, snrs, 100_003, 40_000, seed=7, rank=0, world=1).run()
+    parts = [SCMonteCarlo(code, snrs, 100_003, 40_000, seed=7, rank=r, world=3).run() for r in range(3)]
+    assert [sum(p.bit_errors[i] for p in parts) for i in range(3)] == one.bit_errors
+    assert [sum(p.block_errors[i] for p in parts) for i in range(3)] == one.block_errors
+
+
+def test_montecarlo_pac_and_gru_drivers_run():
+    import argparse
+    from neural_polar_decoder_amd import PAC, reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import GRUMonteCarlo, SCMonteCarlo
+    from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
+    pac = PAC(argparse.Namespace(target_K=64), 128, 64, 91)
+    r = SCMonteCarlo(pac, [2.0], 20_000, 8192).run()
+    assert 0 < r.ber[0] < 0.2
+    code = reference_polar_code(64, 32)
+    torch.manual_seed(0)
+    net = RNN_Model("GRU", 66, 64, 1, 2, 64, 0, 0).to(DEV)
+    dec = RNN_decoder("y_input", 64, code.info_positions, onehot=True)
+    g = GRUMonteCarlo(code, net, dec, [0.0, 4.0], 2048, 1024).run()
+    assert all(0.3 < b < 0.7 for b in g.ber)  # untrained weights: coin flips
