@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gru", action="store_true", help="skip the secondary CRISP-GRU measurement")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
+    ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -126,8 +128,63 @@ def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
             "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input"}
 
 
+KERNEL_NAME = "sc_fast_kernel<64>"
+
+
+def traffic_child(args):
+    """Child process under rocprofv3 --pmc: a few decode launches of the timed configuration."""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from neural_polar_decoder_amd import reference_polar_code
+    code = reference_polar_code(N_CODE, K_CODE)
+    B = args.batch
+    _, _, y = code.mc_generate(B, 2.0, SEED, 2, 0, device=dev, want_msg=False)
+    hat = torch.empty(B, K_CODE, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    for _ in range(4):
+        code.sc_decode_mc(y, 2.0, SEED, 0, cnt, msg_hat=hat)
+    torch.cuda.synchronize()
+
+
+def pmc_traffic(args, timeout_s=240):
+    """HBM bytes per decode launch from rocprofv3 PMC counters, one counter per pass
+    (MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of wide coalesced streaming reads on
+    gfx950 -> doubled; WRITE_SIZE exact for 16-B/lane streaming stores; both in KiB)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="npd_pmc_")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, ctr)
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p", "--", sys.executable,
+               os.path.abspath(__file__), "--traffic-child", "--batch", str(args.batch)]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env, cwd=ROOT)
+        except Exception as e:  # noqa: BLE001
+            return None, f"rocprofv3 failed: {e}"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return None, f"rocprofv3 rc={r.returncode}"
+        xs = [float(row["Counter_Value"]) for row in csv.DictReader(open(files[0]))
+              if KERNEL_NAME.split("<")[0] in row["Kernel_Name"] and row["Counter_Name"] == ctr]
+        if not xs:
+            return None, "kernel not found in PMC output"
+        vals[ctr] = sum(xs[1:]) / max(1, len(xs) - 1) if len(xs) > 1 else xs[0]  # skip the first (cold) launch
+    shutil.rmtree(tmp, ignore_errors=True)
+    return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024, "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 read)"
+
+
 def main():
     args = parse()
+    if args.traffic_child:
+        return traffic_child(args)
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", torch.cuda.current_device())
     from neural_polar_decoder_amd import reference_polar_code
@@ -206,7 +263,7 @@ def main():
                    "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "sc_decode_kernel<64,64,polar> (npd_sc_decode_mc)",
+                     "kernel": KERNEL_NAME + " (npd_sc_decode_mc)",
                      "algorithmic_bytes_per_launch": BYTES_PER_CW * B, "avg_launch_ms": avg_launch_s * 1e3},
         "ber": {str(s): ber[s] for s in snrs},
         "bler": {str(s): bler[s] for s in snrs},
@@ -214,6 +271,10 @@ def main():
     }
     if not args.no_gru:
         out["crisp_gru"] = gru_measure(code, dev, ys[2], snrs[2])
+    if not args.no_traffic and world == 1:
+        traffic, how = pmc_traffic(args)
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic_source"] = how
     if not args.no_cpu_baseline:
         ys_host = [y[: 1 << 18].cpu().numpy() for y in ys]
         out["cpu_baseline"] = cpu_baseline(ys_host, snrs, code.info_positions, args.cpu_seconds)

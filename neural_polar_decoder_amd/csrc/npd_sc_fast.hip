@@ -12,6 +12,23 @@
 //     Philox message bits, and msg_hat leaves as coalesced 16-B stores.
 #include "npd_common.hpp"
 
+// Tuning knobs (compile-time; defaults are the measured best on MI355X):
+#ifndef NPD_SCF_WPE
+#define NPD_SCF_WPE 2
+#endif
+#ifndef NPD_SCF_BRANCHFREE
+#define NPD_SCF_BRANCHFREE 0
+#endif
+#ifndef NPD_SCF_DIRECT
+#define NPD_SCF_DIRECT 0  // 1: each lane loads its own row (no LDS transpose; uncoalesced 16-B pieces)
+#endif
+#ifndef NPD_SCF_ROOT_LDS
+#define NPD_SCF_ROOT_LDS 0  // 1: the root level is read from the LDS row image instead of 64 VGPRs
+#endif
+#ifndef NPD_SCF_PREFETCH
+#define NPD_SCF_PREFETCH 1
+#endif
+
 namespace npd {
 namespace scf {
 
@@ -51,14 +68,29 @@ struct Lane {
     float beta[N];
     char* lds;
     uint32_t u_row;    // byte address of this lane's decision row (slot order)
+    uint32_t slot;     // wave-uniform running rank of the next information position
+    uint32_t fz[(N + 31) / 32];  // frozen-position bits (re-materialised each tile, see below)
+    float infty;
 };
 
 template <int N, int I>
 __device__ __forceinline__ void leaf(Lane<N>& c, const CodeParams& p, float L) {
-    const bool frozen = (p.frozen[I >> 5] >> (I & 31)) & 1u;
-    const float lf = L + (frozen ? p.infty : 0.0f);  // polar.py:438/446
+    const bool frozen = (c.fz[I >> 5] >> (I & 31)) & 1u;
+    const float lf = L + (frozen ? c.infty : 0.0f);  // polar.py:438/446
     const float u = sgn_bits(lf);                     // polar.py:479
-    if (!frozen) *reinterpret_cast<int8_t*>(c.lds + c.u_row + p.rank[I]) = (int8_t)(int)u;
+#if NPD_SCF_BRANCHFREE
+    // branch-free: frozen decisions go to the row's padding byte (NB - 1 >= N); one basic block, but
+    // the scheduler then keeps more values live (more VGPRs) -- measured slower at 2 waves/SIMD
+    constexpr uint32_t kPad = 4 * ((N / 4) | 1) - 1;
+    const uint32_t off = frozen ? kPad : c.slot;
+    *reinterpret_cast<int8_t*>(c.lds + c.u_row + off) = (int8_t)(int)u;
+    c.slot += frozen ? 0u : 1u;
+#else
+    if (!frozen) {
+        *reinterpret_cast<int8_t*>(c.lds + c.u_row + c.slot) = (int8_t)(int)u;
+        ++c.slot;
+    }
+#endif
     c.beta[I] = u;
 }
 
@@ -100,14 +132,94 @@ __device__ __forceinline__ uint32_t nz_bytes(uint32_t x) {
     return (uint32_t)__builtin_popcount(t & 0x80808080u);
 }
 
+// Root node with its input level (the received word, scaled) read from the lane's swizzled LDS row
+// twice -- for f and for g -- instead of being held in VGPRs across the whole left subtree.
 template <int N>
-__global__ __launch_bounds__(64) void sc_fast_kernel(const CodeParams p, const Args a) {
+__device__ __forceinline__ void root_lds(Lane<N>& c, const CodeParams& p, const char* lds, uint32_t row_chunk, int sw,
+                                         float scale) {
+    constexpr int C = N / 4, h = N / 2;
+    constexpr int n = log2c<N>();
+#pragma unroll
+    for (int q = 0; q < C / 2; ++q) {
+        const f4 A = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)(q ^ sw)));
+        const f4 Bv = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)((q + C / 2) ^ sw)));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) c.lv[h + 4 * q + e] = f_minsum(rmul(scale, A[e]), rmul(scale, Bv[e]));
+    }
+    node<N, n - 1, 0>(c, p);
+#pragma unroll
+    for (int q = 0; q < C / 2; ++q) {
+        const f4 A = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)(q ^ sw)));
+        const f4 Bv = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)((q + C / 2) ^ sw)));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            c.lv[h + 4 * q + e] = c.beta[4 * q + e] * rmul(scale, A[e]) + rmul(scale, Bv[e]);
+    }
+    node<N, n - 1, h>(c, p);
+}
+
+// msg_hat of one finished tile: its rows*K floats are contiguous in HBM; decisions are int8 in slot order
+template <int N>
+__device__ __forceinline__ void store_msg(const char* lds, uint32_t kU, float* msg, int64_t row0, int rows, int K,
+                                          int lane) {
+    constexpr int NB = 4 * ((N / 4) | 1);
+    float* dst = msg + row0 * (int64_t)K;
+    const int total = rows * K;
+    if ((K & 3) == 0) {
+        int f = 4 * lane;
+        int r = f / K, col = f % K;
+        const int dr = 256 / K, dc = 256 % K;
+        for (; f < total; f += 256) {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(lds + kU + (uint32_t)(r * NB + col));
+            f4 o;
+            o.x = (float)(int8_t)(w & 0xFFu);
+            o.y = (float)(int8_t)((w >> 8) & 0xFFu);
+            o.z = (float)(int8_t)((w >> 16) & 0xFFu);
+            o.w = (float)(int8_t)(w >> 24);
+            *reinterpret_cast<f4*>(dst + f) = o;
+            r += dr;
+            col += dc;
+            if (col >= K) {
+                col -= K;
+                ++r;
+            }
+        }
+    } else {
+        int r = lane / K, col = lane % K;
+        const int dr = kWave / K, dc = kWave % K;
+        for (int f = lane; f < total; f += kWave) {
+            dst[f] = (float)*reinterpret_cast<const int8_t*>(lds + kU + (uint32_t)(r * NB + col));
+            r += dr;
+            col += dc;
+            if (col >= K) {
+                col -= K;
+                ++r;
+            }
+        }
+    }
+}
+
+#ifdef NPD_SCF_STAMPS
+// diagnostic build only: per-phase cycle sums per wave, written to counters + 2 (never in the product)
+#define STAMP(var)                                                                     \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        unsigned long long _t;                                                         \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");    \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        var = _t;                                                                      \
+    } while (0)
+#else
+#define STAMP(var) do { } while (0)
+#endif
+template <int N>
+__global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
     constexpr int C = N / 4;                 // 16-B chunks per row (and per lane per tile)
     constexpr int NB = 4 * ((N / 4) | 1);    // decision-row stride in bytes (odd dword count)
     constexpr uint32_t kStage = 0;
-    constexpr uint32_t kU = kWave * N * 4;
+    constexpr uint32_t kU = NPD_SCF_DIRECT ? 0u : (uint32_t)(kWave * N * 4);
     const int lane = threadIdx.x;
     const int K = p.K;
 
@@ -122,17 +234,38 @@ __global__ __launch_bounds__(64) void sc_fast_kernel(const CodeParams p, const A
 
     // prefetch registers: chunk q of tile t for this lane = float4 index t*64*C + lane + 64*q
     f4 nx[C];
+    int64_t pend_row0 = 0;  // previous tile: its msg_hat stores are issued one iteration late, before the
+    int pend_rows = 0;      // next prefetch, so the wait for that prefetch never waits for fresh stores
     int64_t t = blockIdx.x;
-    if (t < a.ntiles) {
+    if (NPD_SCF_PREFETCH && t < a.ntiles) {
 #pragma unroll
         for (int q = 0; q < C; ++q) {
             int64_t gi = t * (int64_t)(kWave * C) + lane + kWave * q;
             nx[q] = y4[gi < last4 ? gi : last4];
         }
     }
+    unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0;
+    unsigned long long ph[4] = {0, 0, 0, 0};
     for (; t < a.ntiles; t += gridDim.x) {
+        STAMP(ts0);
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
+        if (!NPD_SCF_PREFETCH) {
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                int64_t gi = NPD_SCF_DIRECT ? (t * kWave + lane) * C + q : t * (int64_t)(kWave * C) + lane + kWave * q;
+                nx[q] = y4[gi < last4 ? gi : last4];
+            }
+        }
+        if (NPD_SCF_DIRECT) {
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                c.lv[N + 4 * q + 0] = rmul(a.scale, nx[q].x);
+                c.lv[N + 4 * q + 1] = rmul(a.scale, nx[q].y);
+                c.lv[N + 4 * q + 2] = rmul(a.scale, nx[q].z);
+                c.lv[N + 4 * q + 3] = rmul(a.scale, nx[q].w);
+            }
+        } else {
         // ---- transpose the tile through LDS: chunk (lane + 64q) -> row r = (lane + 64q)/C, col chunk
 #pragma unroll
         for (int q = 0; q < C; ++q) {
@@ -140,26 +273,49 @@ __global__ __launch_bounds__(64) void sc_fast_kernel(const CodeParams p, const A
             const int r = pch / C, cc = pch % C;
             *reinterpret_cast<f4*>(lds + kStage + 16u * (uint32_t)(r * C + (cc ^ swz<C>(r)))) = nx[q];
         }
-#pragma unroll
-        for (int q = 0; q < C; ++q) {
-            const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
-            c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
-            c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
-            c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
-            c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
-        }
-        // ---- prefetch the next tile (lands while this one is decoded)
-        const int64_t tn = t + gridDim.x;
-        if (tn < a.ntiles) {
+        if (!NPD_SCF_ROOT_LDS) {
 #pragma unroll
             for (int q = 0; q < C; ++q) {
-                int64_t gi = tn * (int64_t)(kWave * C) + lane + kWave * q;
+                const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
+                c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
+                c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
+                c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
+                c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+            }
+        }
+        }
+        STAMP(ts1);
+        // ---- previous tile's msg_hat (its decision rows are read before this tile's leaves overwrite them)
+        if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane);
+        // ---- prefetch the next tile (lands while this one is decoded)
+        const int64_t tn = t + gridDim.x;
+        if (NPD_SCF_PREFETCH && tn < a.ntiles) {
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                int64_t gi = NPD_SCF_DIRECT ? (tn * kWave + lane) * C + q : tn * (int64_t)(kWave * C) + lane + kWave * q;
                 nx[q] = y4[gi < last4 ? gi : last4];
             }
         }
-        // ---- decode
-        node<N, n, 0>(c, p);
+        STAMP(ts2);
+        // ---- decode.  The per-leaf frozen tests are loop-invariant; left alone the compiler hoists all
+        // of them out of the tile loop and spills the resulting 64 SGPR pairs to VGPR lanes.  Making the
+        // frozen words opaque per tile keeps each test a single s_bitcmp next to its leaf.
+#pragma unroll
+        for (int w = 0; w < (N + 31) / 32; ++w) {
+            uint32_t fw = p.frozen[w];
+            asm volatile("" : "+s"(fw));
+            c.fz[w] = fw;
+        }
+        {
+            float inf = p.infty;
+            asm volatile("" : "+s"(inf));
+            c.infty = inf;
+        }
+        c.slot = 0;
+        if (NPD_SCF_ROOT_LDS && !NPD_SCF_DIRECT) root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, a.scale);
+        else node<N, n, 0>(c, p);
 
+        STAMP(ts3);
         // ---- error count: 4 slots per dword vs the Philox message bits (errors_ber/bler semantics)
         if (a.count) {
             const uint64_t cw = a.cw_offset + (uint64_t)(row0 + lane);
@@ -184,44 +340,22 @@ __global__ __launch_bounds__(64) void sc_fast_kernel(const CodeParams p, const A
             }
         }
 
-        // ---- msg_hat: the tile's rows*K floats are contiguous in HBM
-        if (a.msg) {
-            float* dst = a.msg + row0 * (int64_t)K;
-            const int total = rows * K;
-            if ((K & 3) == 0) {
-                int f = 4 * lane;
-                int r = f / K, col = f % K;
-                const int dr = 256 / K, dc = 256 % K;
-                for (; f < total; f += 256) {
-                    const uint32_t w = *reinterpret_cast<const uint32_t*>(lds + kU + (uint32_t)(r * NB + col));
-                    f4 o;
-                    o.x = (float)(int8_t)(w & 0xFFu);
-                    o.y = (float)(int8_t)((w >> 8) & 0xFFu);
-                    o.z = (float)(int8_t)((w >> 16) & 0xFFu);
-                    o.w = (float)(int8_t)(w >> 24);
-                    *reinterpret_cast<f4*>(dst + f) = o;
-                    r += dr;
-                    col += dc;
-                    if (col >= K) {
-                        col -= K;
-                        ++r;
-                    }
-                }
-            } else {
-                int r = lane / K, col = lane % K;
-                const int dr = kWave / K, dc = kWave % K;
-                for (int f = lane; f < total; f += kWave) {
-                    dst[f] = (float)*reinterpret_cast<const int8_t*>(lds + kU + (uint32_t)(r * NB + col));
-                    r += dr;
-                    col += dc;
-                    if (col >= K) {
-                        col -= K;
-                        ++r;
-                    }
-                }
-            }
-        }
+        STAMP(ts4);
+        ph[0] += ts1 - ts0;  // wait for the tile + transpose
+        ph[1] += ts2 - ts1;  // previous tile's stores + prefetch issue
+        ph[2] += ts3 - ts2;  // SC decode
+        ph[3] += ts4 - ts3;  // error count
+        pend_row0 = row0;
+        pend_rows = rows;
     }
+#ifdef NPD_SCF_STAMPS
+    if (lane == 0 && a.counters) {
+        for (int i = 0; i < 4; ++i) atomicAdd(a.counters + 2 + i, ph[i]);
+        atomicAdd(a.counters + 6, 1ull);
+    }
+#endif
+    // the last tile's msg_hat
+    if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane);
 
     if (a.count) {
         const uint32_t eb = wave_sum_u32(err_bits);
@@ -236,7 +370,7 @@ __global__ __launch_bounds__(64) void sc_fast_kernel(const CodeParams p, const A
 template <int N>
 static int launch(const CodeParams& p, Args a, hipStream_t s) {
     constexpr int NB = 4 * ((N / 4) | 1);
-    const size_t lds = (size_t)kWave * N * 4 + (size_t)kWave * NB;
+    const size_t lds = (NPD_SCF_DIRECT ? 0 : (size_t)kWave * N * 4) + (size_t)kWave * NB;
     a.ntiles = (a.B + kWave - 1) / kWave;
     auto kern = sc_fast_kernel<N>;
     int occ = 0;
