@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gru", action="store_true", help="skip the secondary CRISP-GRU measurement")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
+    ap.add_argument("--no-conv", action="store_true", help="skip the secondary conv-model measurement")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -138,6 +139,32 @@ def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
 
 
 KERNEL_NAME = "sc_fast_kernel<64>"
+
+
+def conv_measure(dev, batch=8192, iters=3):
+    """Secondary line (configs[4], per GPU): Polar(256,128) convNet decoder, embed 128 (run_alt.sh),
+    seeded random weights, fp32 MFMA kernels."""
+    import argparse as _ap
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.models import convNet
+    torch.manual_seed(0)
+    net = convNet(_ap.Namespace(embed_dim=128, max_len=256, N=256, dont_use_bias=False, dropout=0.0)).to(dev).eval()
+    code = reference_polar_code(256, 128)
+    _, _, y = code.mc_generate(batch, 1.0, SEED, 0, 0, device=dev, want_msg=False)
+    net.logits(y)  # warm + weight packing
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        net.logits(y)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    flop_cw = 258.8e6  # SURVEY.md 8(d): 2 x (95.5 M conv + 33.9 M FC) MAC
+    tf = flop_cw * batch / (ms / 1e3) / 1e12
+    return {"value": batch / (ms / 1e3), "unit": "codewords/s", "batch": batch, "avg_forward_ms": ms,
+            "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": tf, "peak_tflops_fp32": 157.3,
+            "frac": tf / 157.3, "config": "configs[4] per GPU: Polar(256,128) convNet embed 128"}
 
 
 def traffic_child(args):
@@ -280,6 +307,8 @@ def main():
     }
     if not args.no_gru:
         out["crisp_gru"] = gru_measure(code, dev, ys[2], snrs[2])
+    if not args.no_conv:
+        out["conv_model"] = conv_measure(dev)
     if not args.no_traffic and world == 1:
         traffic, how = pmc_traffic(args)
         out["roofline"]["traffic"] = traffic

@@ -1,0 +1,386 @@
+// npd_conv.hip -- convNet decoder (models.py:691-772) on MFMA.
+//
+// Reference forward (models.py:742-767): 10 dilated Conv1d(k=7) + GELU with three residual blocks,
+// flatten (c*N + l), Linear(E*N -> 4N) + GELU, Linear(4N -> N) + GELU, Linear(N -> N), Dropout (eval:
+// identity), LayerNorm(N, eps 1e-6), decisions = sign(logits).
+//
+// MI355X mapping (fp32 path, v_mfma_f32_32x32x2_f32, exact fp32 FMA chains):
+//   * conv layer = implicit GEMM  out[co][l] = sum_{t,ci} W[co][ci][t] * in[ci][l + d(t-3)]:
+//     MFMA rows = output channels (A = weights, pre-permuted on the host into A-operand order,
+//     k = t*Cin + ci), columns = positions (B = the input slab staged in LDS with its zero halo);
+//     the epilogue fuses bias + GELU (+ residual) and writes 32 consecutive positions per register.
+//   * FC layers = LDS-tiled GEMM with MFMA rows = codewords, columns = output features (so the
+//     epilogue writes contiguous feature runs), bias + GELU fused.
+//   * LayerNorm + sign: one wave per codeword.
+// Activations of a chunk of codewords live in a caller-provided workspace (row-major (B, C, N)).
+#include <math.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "npd_common.hpp"
+
+namespace npd {
+namespace conv {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int kLayers = 10;
+constexpr int kChunk = 4096;  // codewords per pass through the layer pipeline
+
+struct LayerDesc {
+    int cin, cout, dil;
+    int res;        // 1: add the block input (residual) after GELU
+    int64_t woff;   // offset (floats) of the permuted weights in the device image
+    int64_t boff;   // offset of the bias
+    int ksteps;     // ceil(7*cin / 2)
+};
+
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+
+__device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------ conv layer
+// grid: (N/64 position tiles, cout/64 channel tiles, codewords); block 256 = 2 (co) x 2 (pos) waves
+__global__ __launch_bounds__(256) void conv_layer_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                         const float* __restrict__ res, const float* __restrict__ wimg,
+                                                         const float* __restrict__ bias, int cin, int cout, int N,
+                                                         int dil, int ksteps, int do_res) {
+    extern __shared__ __attribute__((aligned(16))) float slab[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int l0 = blockIdx.x * 64;
+    const int co_tile = blockIdx.y;  // 64 output channels
+    const int64_t b = blockIdx.z;
+    const int halo = 3 * dil;
+    const int W = 64 + 2 * halo;
+    const int WS = W + 1;
+    const float* inb = in + b * (int64_t)cin * N;
+    for (int e = tid; e < cin * W; e += 256) {
+        const int ci = e / W, p = e - ci * W;
+        const int l = l0 - halo + p;
+        slab[ci * WS + p] = (l >= 0 && l < N) ? inb[(int64_t)ci * N + l] : 0.0f;
+    }
+    __syncthreads();
+    const int co_sub = wave & 1, pos_sub = wave >> 1;
+    const int co_t32 = co_tile * 2 + co_sub;  // 32-channel tile index
+    const f4* wq = reinterpret_cast<const f4*>(wimg) + (int64_t)co_t32 * ((ksteps + 3) / 4) * 64 + lane;
+    f16v acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // lane's running (tap, channel) of k = 2s + h
+    int t = 0, ci = h;
+    while (ci >= cin) { ci -= cin; ++t; }
+    const int pcol = pos_sub * 32 + col;
+    const int ng = (ksteps + 3) / 4;
+    f4 wn = wq[0];
+    for (int g = 0; g < ng; ++g) {
+        const f4 w = wn;
+        if (g + 1 < ng) wn = wq[(g + 1) * 64];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool valid = t < 7;
+            const float bv = valid ? slab[ci * WS + pcol + dil * t] : 0.0f;
+            acc = mfma(w[e], bv, acc);
+            ci += 2;
+            while (ci >= cin) {
+                ci -= cin;
+                ++t;
+            }
+        }
+    }
+    // epilogue: rows = channels, columns = positions
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int co = co_t32 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int l = l0 + pcol;
+        if (co < cout) {
+            const int64_t o = (b * cout + co) * (int64_t)N + l;
+            float v = gelu(acc[r] + bias[co]);
+            if (do_res) v += res[o];
+            out[o] = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ FC GEMM
+// out[m][j] = act(sum_k X[m][k] * Wt[j][k] + bias[j]);  block tile 64 (m) x 64 (j), K step 32.
+constexpr int GK = 32;
+constexpr int GS = GK + 1;  // padded LDS row (floats): conflict-free column reads
+
+__global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, const float* __restrict__ Wt,
+                                                 const float* __restrict__ bias, float* __restrict__ out, int M, int K,
+                                                 int Nout, int act) {
+    __shared__ float As[2][64 * GS];
+    __shared__ float Bs[2][64 * GS];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int m0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+    const int msub = wave & 1, jsub = wave >> 1;
+    // loader mapping: 64 rows x 32 k = 512 float4 per operand; thread loads 2 float4 of A and of B
+    auto load = [&](int buf, int k0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = tid + 256 * u;  // 0..511
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            int mr = m0 + r;
+            if (mr >= M) mr = M - 1;
+            const f4 a = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
+            const f4 w = *reinterpret_cast<const f4*>(Wt + (int64_t)(j0 + r) * K + k0 + c4);
+            float* as = &As[buf][r * GS + c4];
+            float* bs = &Bs[buf][r * GS + c4];
+            as[0] = a.x; as[1] = a.y; as[2] = a.z; as[3] = a.w;
+            bs[0] = w.x; bs[1] = w.y; bs[2] = w.z; bs[3] = w.w;
+        }
+    };
+    f16v acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nk = K / GK;
+    load(0, 0);
+    __syncthreads();
+    for (int kb = 0; kb < nk; ++kb) {
+        const int cur = kb & 1;
+        if (kb + 1 < nk) load(cur ^ 1, (kb + 1) * GK);
+        const float* as = &As[cur][(msub * 32 + col) * GS + h];
+        const float* bs = &Bs[cur][(jsub * 32 + col) * GS + h];
+#pragma unroll
+        for (int s = 0; s < GK / 2; ++s) acc = mfma(as[2 * s], bs[2 * s], acc);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + msub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int j = j0 + jsub * 32 + col;
+        if (m < M) {
+            float v = acc[r] + bias[j];
+            if (act) v = gelu(v);
+            out[(int64_t)m * Nout + j] = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ LayerNorm + sign
+__global__ __launch_bounds__(256) void layernorm_sign_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                             const float* __restrict__ be, float* __restrict__ logits,
+                                                             float* __restrict__ dec, int M, int N) {
+    const int lane = threadIdx.x & 63;
+    const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= M) return;
+    const float* r = x + m * N;
+    float s = 0.0f;
+    for (int i = lane; i < N; i += 64) s += r[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)N;
+    float v = 0.0f;
+    for (int i = lane; i < N; i += 64) {
+        const float d = r[i] - mean;
+        v += d * d;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const float rstd = 1.0f / sqrtf(v / (float)N + 1e-6f);
+    for (int i = lane; i < N; i += 64) {
+        const float y = (r[i] - mean) * rstd * g[i] + be[i];
+        if (logits) logits[m * N + i] = y;
+        if (dec) dec[m * N + i] = y > 0.0f ? 1.0f : (y < 0.0f ? -1.0f : 0.0f);
+    }
+}
+
+}  // namespace conv
+}  // namespace npd
+
+using namespace npd;
+using namespace npd::conv;
+
+struct npd_conv {
+    int N, E, precision, device;
+    LayerDesc layers[kLayers];
+    float* img;         // device: permuted conv weights + biases + FC weights/biases + LN params
+    int64_t off_fc[3][2];  // (weight, bias) offsets of the three Linear layers
+    int64_t off_ln[2];
+};
+
+static void conv_spec(int E, int idx, int& cin, int& cout, int& dil, int& res) {
+    const int H = E / 2;
+    // (cin, cout, dilation, residual-after) for layers1.0, layers1.2, layers2.0, ..., layers5.2
+    static const int dils[kLayers] = {1, 2, 4, 1, 2, 4, 1, 2, 4, 1};
+    dil = dils[idx];
+    cin = idx == 0 ? 1 : (idx == 9 ? E : H);
+    cout = idx >= 8 ? E : H;
+    res = (idx == 3 || idx == 5 || idx == 7) ? 1 : 0;
+}
+
+extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n_weights, int precision,
+                               npd_conv** out) {
+    NPD_ARG(out != nullptr, "npd_conv_create: out is NULL");
+    *out = nullptr;
+    NPD_ARG(weights != nullptr, "npd_conv_create: weights is NULL");
+    NPD_ARG(N >= 64 && N <= 1024 && N % 64 == 0, "npd_conv_create: N must be a multiple of 64 in [64, 1024]");
+    NPD_ARG(embed >= 2 && embed <= 512 && embed % 2 == 0, "npd_conv_create: embed must be even, in [2, 512]");
+    NPD_ARG(precision == 0, "npd_conv_create: only fp32 (precision 0) is built");
+    const int E = embed;
+    // host weights in state_dict order: (w, b) per conv layer, then 3 x (w, b) Linear, then LN (g, b)
+    int64_t expect = 0;
+    for (int i = 0; i < kLayers; ++i) {
+        int ci, co, d, r;
+        conv_spec(E, i, ci, co, d, r);
+        expect += (int64_t)co * ci * 7 + co;
+    }
+    expect += (int64_t)4 * N * E * N + 4 * N + (int64_t)N * 4 * N + N + (int64_t)N * N + N + 2 * N;
+    NPD_ARG(n_weights == expect, "npd_conv_create: weight count does not match (N, embed)");
+    npd_conv* c = new (std::nothrow) npd_conv;
+    if (!c) return fail(NPD_ENOMEM, "npd_conv_create: out of memory");
+    memset(c, 0, sizeof(*c));
+    c->N = N;
+    c->E = E;
+    c->precision = precision;
+    std::vector<float> img;
+    const float* p = weights;
+    for (int i = 0; i < kLayers; ++i) {
+        int ci, co, d, r;
+        conv_spec(E, i, ci, co, d, r);
+        LayerDesc& L = c->layers[i];
+        L.cin = ci; L.cout = co; L.dil = d; L.res = r;
+        L.ksteps = (7 * ci + 1) / 2;
+        const int ng = (L.ksteps + 3) / 4;
+        // pad channel tiles to 64 so every (64-channel) block has two 32-row MFMA tiles
+        const int co_pad = ((co + 63) / 64) * 64;
+        L.woff = (int64_t)img.size();
+        img.resize(img.size() + (size_t)(co_pad / 32) * ng * 64 * 4, 0.0f);
+        const float* w = p;  // (co, ci, 7)
+        for (int t32 = 0; t32 < co_pad / 32; ++t32)
+            for (int s = 0; s < L.ksteps; ++s)
+                for (int l = 0; l < 64; ++l) {
+                    const int row = 32 * t32 + (l & 31);
+                    const int k = 2 * s + (l >> 5);
+                    float v = 0.0f;
+                    if (row < co && k < 7 * ci) {
+                        const int t = k / ci, cc = k % ci;
+                        v = w[((int64_t)row * ci + cc) * 7 + t];
+                    }
+                    img[L.woff + (((int64_t)t32 * ng + s / 4) * 64 + l) * 4 + (s & 3)] = v;
+                }
+        p += (int64_t)co * ci * 7;
+        L.boff = (int64_t)img.size();
+        img.insert(img.end(), p, p + co);
+        img.resize(L.boff + co_pad, 0.0f);
+        p += co;
+    }
+    const int64_t fcin[3] = {(int64_t)E * N, 4 * N, N}, fcout[3] = {4 * N, N, N};
+    for (int f = 0; f < 3; ++f) {
+        while (img.size() % 4) img.push_back(0.0f);  // 16-B alignment for f4 loads
+        c->off_fc[f][0] = (int64_t)img.size();
+        img.insert(img.end(), p, p + fcin[f] * fcout[f]);
+        p += fcin[f] * fcout[f];
+        c->off_fc[f][1] = (int64_t)img.size();
+        img.insert(img.end(), p, p + fcout[f]);
+        p += fcout[f];
+    }
+    c->off_ln[0] = (int64_t)img.size();
+    img.insert(img.end(), p, p + N);
+    p += N;
+    c->off_ln[1] = (int64_t)img.size();
+    img.insert(img.end(), p, p + N);
+    hipError_t e = hipGetDevice(&c->device);
+    if (e == hipSuccess) e = hipMalloc(&c->img, img.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(c->img, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (c->img) (void)hipFree(c->img);
+        delete c;
+        return hip_fail(e, "npd_conv_create");
+    }
+    *out = c;
+    return NPD_OK;
+}
+
+extern "C" int npd_conv_destroy(npd_conv* c) {
+    if (!c) return NPD_OK;
+    if (c->img) (void)hipFree(c->img);
+    delete c;
+    return NPD_OK;
+}
+
+static int64_t chunk_of(int64_t B) { return B < kChunk ? B : kChunk; }
+
+extern "C" int64_t npd_conv_workspace_bytes(const npd_conv* c, int64_t B) {
+    if (!c || B <= 0) return 0;
+    const int64_t Bc = chunk_of(B);
+    // three activation buffers of (Bc, E, N) + FC1/FC2/FC3 outputs
+    return (3 * Bc * (int64_t)c->E * c->N + Bc * 4 * (int64_t)c->N + 2 * Bc * (int64_t)c->N) * 4 + 256;
+}
+
+extern "C" int npd_conv_forward(const npd_conv* c, const float* y, float* logits, float* decoded, void* workspace,
+                                int64_t B, void* stream) {
+    NPD_ARG(c != nullptr, "npd_conv_forward: conv is NULL");
+    NPD_ARG(B >= 0, "npd_conv_forward: B < 0");
+    if (B == 0) return NPD_OK;
+    NPD_ARG(y != nullptr && workspace != nullptr, "npd_conv_forward: null pointer");
+    NPD_ARG(logits != nullptr || decoded != nullptr, "npd_conv_forward: nothing to write");
+    hipStream_t s = (hipStream_t)stream;
+    const int N = c->N, E = c->E;
+    const int64_t Bc = chunk_of(B);
+    float* ws = reinterpret_cast<float*>(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    float* A0 = ws;
+    float* A1 = A0 + Bc * (int64_t)E * N;
+    float* A2 = A1 + Bc * (int64_t)E * N;
+    float* H1 = A2 + Bc * (int64_t)E * N;
+    float* H2 = H1 + Bc * 4 * (int64_t)N;
+    float* H3 = H2 + Bc * (int64_t)N;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    for (int64_t b0 = 0; b0 < B; b0 += Bc) {
+        const int64_t nb = (B - b0) < Bc ? (B - b0) : Bc;
+        // layer inputs/outputs: x (N floats per cw) -> A0 -> A1 -> ... ; block inputs kept for the residual
+        const float* src = y + b0 * N;
+        // buffers: cur input, output, residual source
+        float* bufs[3] = {A0, A1, A2};
+        int in_idx = -1;   // -1: y
+        int res_idx = -1;  // buffer holding the current block input
+        int out_idx = 0;
+        for (int i = 0; i < kLayers; ++i) {
+            const LayerDesc& L = c->layers[i];
+            const float* in = in_idx < 0 ? src : bufs[in_idx];
+            // choose an output buffer that is neither the input nor the pending residual
+            out_idx = 0;
+            while (out_idx == in_idx || out_idx == res_idx) ++out_idx;
+            float* o = bufs[out_idx];
+            const float* rsrc = L.res ? bufs[res_idx] : nullptr;
+            const int halo = 3 * L.dil;
+            const size_t lds = (size_t)L.cin * (64 + 2 * halo + 1) * 4;
+            dim3 grid(N / 64, (L.cout + 63) / 64, (unsigned)nb);
+            hipLaunchKernelGGL(conv_layer_kernel, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff, c->img + L.boff,
+                               L.cin, L.cout, N, L.dil, L.ksteps, L.res);
+            int rc = launch_check("conv_layer_kernel launch");
+            if (rc) return rc;
+            // block structure (models.py:742-766): the output of layers1 (i == 1) and of each residual
+            // block (i == 3, 5, 7) is the next block's input and residual
+            if (i == 1 || i == 3 || i == 5 || i == 7) res_idx = out_idx;
+            in_idx = out_idx;
+        }
+        const float* flat = bufs[in_idx];  // (nb, E*N): c*N + l, as torch.flatten(start_dim=1)
+        const int64_t K1 = (int64_t)E * N;
+        dim3 g1(4 * N / 64, (unsigned)((nb + 63) / 64));
+        hipLaunchKernelGGL(fc_kernel, g1, dim3(256), 0, s, flat, c->img + c->off_fc[0][0], c->img + c->off_fc[0][1], H1,
+                           (int)nb, (int)K1, 4 * N, 1);
+        int rc = launch_check("fc_kernel launch");
+        if (rc) return rc;
+        dim3 g2(N / 64, (unsigned)((nb + 63) / 64));
+        hipLaunchKernelGGL(fc_kernel, g2, dim3(256), 0, s, H1, c->img + c->off_fc[1][0], c->img + c->off_fc[1][1], H2,
+                           (int)nb, 4 * N, N, 1);
+        hipLaunchKernelGGL(fc_kernel, g2, dim3(256), 0, s, H2, c->img + c->off_fc[2][0], c->img + c->off_fc[2][1], H3,
+                           (int)nb, N, N, 0);
+        hipLaunchKernelGGL(layernorm_sign_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, H3,
+                           c->img + c->off_ln[0], c->img + c->off_ln[1], logits ? logits + b0 * N : nullptr,
+                           decoded ? decoded + b0 * N : nullptr, (int)nb, N);
+        rc = launch_check("fc/layernorm launch");
+        if (rc) return rc;
+    }
+    return NPD_OK;
+}
