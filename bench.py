@@ -114,27 +114,40 @@ def cpu_baseline(ys_host, snrs, info, budget_s):
 
 def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
     """Secondary line (configs[2]): CRISP GRU hidden 64, 2 layers, Polar(64,32), fused decode kernel.
-    Seeded random weights (no trained checkpoint ships with the reference)."""
+    Seeded random weights (no trained checkpoint ships with the reference). The fp32 kernel (the
+    reference's arithmetic) is the line's value; the opt-in bf16x3 / bf16 MFMA kernels are timed
+    beside it with their decision agreement against the fp32 path on the same batch."""
     from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
     torch.manual_seed(0)
     net = RNN_Model("GRU", N_CODE + 2, 64, 1, 2, N_CODE, 0, 0).to(dev)
-    dec = RNN_decoder("y_input", N_CODE, code.info_positions, onehot=True)
     yb = y[:batch].contiguous()
-    dec.decode(net, False, yb)  # warm (weights packed once)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        dec.decode(net, False, yb)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / iters
     F, N = 64, N_CODE
     flop_cw = 2 * 3 * F * N + N * (2 * 3 * F * F + 2 * 2 * 3 * F * F + 2 * F)  # SURVEY.md 8(d): 4.751 MFLOP
-    tflops = flop_cw * batch / (ms / 1e3) / 1e12
-    return {"value": batch / (ms / 1e3), "unit": "codewords/s", "batch": batch, "avg_launch_ms": ms,
+    res, ref_dec = {}, None
+    for prec, peak in (("fp32", 157.3), ("bf16x3", 2516.6), ("bf16", 2516.6)):
+        dec = RNN_decoder("y_input", N_CODE, code.info_positions, onehot=True, precision=prec)
+        d0 = dec.decode(net, False, yb)  # warm (weights packed once)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            dec.decode(net, False, yb)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        tflops = flop_cw * batch / (ms / 1e3) / 1e12
+        r = {"value": batch / (ms / 1e3), "avg_launch_ms": ms, "achieved_tflops": tflops, "peak_tflops": peak,
+             "frac": tflops / peak}
+        if ref_dec is None:
+            ref_dec = d0
+        else:
+            r["cw_agreement_vs_fp32"] = (d0 == ref_dec).all(1).float().mean().item()
+        res[prec] = r
+    f = res["fp32"]
+    return {"value": f["value"], "unit": "codewords/s", "batch": batch, "avg_launch_ms": f["avg_launch_ms"],
             "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "algorithmic_flop_per_cw": flop_cw,
-            "achieved_tflops": tflops, "peak_tflops_fp32": 157.3, "frac": tflops / 157.3,
+            "achieved_tflops": f["achieved_tflops"], "peak_tflops_fp32": 157.3, "frac": f["frac"],
+            "bf16x3": res["bf16x3"], "bf16": res["bf16"],
             "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input"}
 
 

@@ -27,6 +27,7 @@ struct npd_gru {
     float* img;   // LDS image (device)
     float* wy;    // y-projection A operands (device)
     int64_t img_floats;
+    int64_t wy_lo;
 };
 
 namespace npd {
@@ -337,6 +338,320 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
     return launch_check("gru_decode_kernel launch");
 }
 
+
+// =============================================================================== bf16 MFMA paths
+// precision 1 = bf16x3 split (a*b ~ ah*bh + ah*bl + al*bh, ~2^-16 relative per product),
+// precision 2 = plain bf16 (fp32 accumulate).  v_mfma_f32_32x32x16_bf16: 16x the fp32 MFMA rate.
+// Same orientation as the fp32 kernel: an h' accumulator tile converts register-for-register into
+// the B fragments of the next step (registers 8s..8s+7 -> k-step s, cdna_hip_programming.md sec. 3).
+// Bias / one-hot / previous-decision terms stay an exact fp32 k-step (v_mfma_f32_32x32x2_f32).
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+template <int F, int L, int SPLIT>
+struct GeoB {
+    static constexpr int TT = 3 * F / 32, HT = F / 32, KB = F / 16;
+    static constexpr int NG = (L == 2) ? 3 : 1;
+    static constexpr int IMG = NG * TT * KB * 64 * 4;  // floats: one 16-B bf16x8 fragment per lane per step
+    static constexpr int NS = SPLIT == 3 ? 2 : 1;      // hi (+ lo) images
+    static constexpr int OFF_X = NS * IMG;
+    static constexpr int OFF_IN = OFF_X + NG * TT * 64;
+    static constexpr int OFF_WL = OFF_IN + HT * 64;
+    static constexpr int TOTAL = OFF_WL + 2 * HT * 16;
+};
+
+struct ArgsB {
+    const float* img;
+    const f4* wy;  // [TT][N/16][64] bf16x8 fragments (hi, then lo for SPLIT 3)
+    const float* y;
+    const float* gt;
+    float* decoded;
+    float* logits;
+    int64_t B;
+    int N;
+    int rev;
+    int onehot;
+    float b_lin;
+    int64_t wy_lo;  // offset (in f4) of the lo Wy image
+    uint32_t info[kMaxWords];
+};
+
+__device__ __forceinline__ f16v mfma16(const bf8& a, const bf8& b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float fast_sigmoid(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896340736f * x));
+}
+__device__ __forceinline__ float fast_tanh(float x) { return fmaf(2.0f, fast_sigmoid(2.0f * x), -1.0f); }
+
+__device__ __forceinline__ void gru_update_fast(f16v& h, const f16v& ar, const f16v& az, const f16v& ain,
+                                                const f16v& ahn) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float r = fast_sigmoid(ar[i]);
+        const float z = fast_sigmoid(az[i]);
+        const float nn = fast_tanh(ain[i] + ahn[i] * r);
+        h[i] = (h[i] - nn) * z + nn;
+    }
+}
+
+// split the state tiles into bf16 B fragments (hi and, for SPLIT 3, lo)
+template <int HT, int SPLIT>
+__device__ __forceinline__ void to_frags(const f16v (&h)[HT], bf8 (&hi)[2 * HT], bf8 (&lo)[2 * HT]) {
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = h[t][8 * s + j];
+                const __bf16 b = (__bf16)v;
+                hi[2 * t + s][j] = b;
+                if (SPLIT == 3) lo[2 * t + s][j] = (__bf16)(v - (float)b);
+            }
+}
+
+template <int TT, int KB, int NT, int SPLIT, int IMG>
+__device__ __forceinline__ void gemm_bf(const f4* __restrict__ smem4, int g, int t0, int lane, f16v (&acc)[NT],
+                                        const bf8 (&hi)[KB], const bf8 (&lo)[KB]) {
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+        bf8 ah[NT], al[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f4 v = smem4[((g * TT + t0 + t) * KB + q) * 64 + lane];
+            ah[t] = __builtin_bit_cast(bf8, v);
+            if (SPLIT == 3) al[t] = __builtin_bit_cast(bf8, smem4[IMG / 4 + ((g * TT + t0 + t) * KB + q) * 64 + lane]);
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            acc[t] = mfma16(ah[t], hi[q], acc[t]);
+            if (SPLIT == 3) {
+                acc[t] = mfma16(ah[t], lo[q], acc[t]);
+                acc[t] = mfma16(al[t], hi[q], acc[t]);
+            }
+        }
+    }
+}
+
+template <int F, int L, int SPLIT>
+__global__ __launch_bounds__(256) void gru_decode_bf_kernel(const ArgsB a) {
+    using G = GeoB<F, L, SPLIT>;
+    constexpr int TT = G::TT, HT = G::HT, KB = G::KB, IMG = G::IMG;
+    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
+    const float* smem = reinterpret_cast<const float*>(smem4);
+    {
+        const f4* src = reinterpret_cast<const f4*>(a.img);
+        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int half = lane >> 5;
+    const int col = lane & 31;
+    const int N = a.N;
+    const int64_t ntiles = (a.B + 31) / 32;
+    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float one_or_zero = half ? 0.0f : 1.0f;
+
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+        const int64_t cw = tile * 32 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        // ---- P = W_ih0[:, :N] . y ; k-step q covers y[16q + 8*half .. +7]
+        f16v P[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) P[t] = zero;
+        {
+            const float* yr = a.y + cwc * N;
+            const int nq = N / 16;
+            for (int q = 0; q < nq; ++q) {
+                const f4 y0 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half);
+                const f4 y1 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half + 4);
+                bf8 yh, yl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float v = j < 4 ? y0[j] : y1[j - 4];
+                    yh[j] = (__bf16)v;
+                    if (SPLIT == 3) yl[j] = (__bf16)(v - (float)yh[j]);
+                }
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const bf8 wh = __builtin_bit_cast(bf8, a.wy[(t * nq + q) * 64 + lane]);
+                    P[t] = mfma16(wh, yh, P[t]);
+                    if (SPLIT == 3) {
+                        const bf8 wl = __builtin_bit_cast(bf8, a.wy[a.wy_lo + (t * nq + q) * 64 + lane]);
+                        P[t] = mfma16(wh, yl, P[t]);
+                        P[t] = mfma16(wl, yh, P[t]);
+                    }
+                }
+            }
+        }
+        f16v h0[HT], h1[HT];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+            h0[t] = zero;
+            h1[t] = zero;
+        }
+        float xb = 1.0f;
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            const float xbe = half ? xb : 1.0f;
+            {
+                bf8 fh[KB], fl[KB];
+                to_frags<HT, SPLIT>(h0, fh, fl);
+                f16v acc[TT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
+#pragma unroll
+                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
+                gemm_bf<TT, KB, TT, SPLIT, IMG>(smem4, 0, 0, lane, acc, fh, fl);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
+                    gru_update_fast(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                }
+            }
+            if constexpr (L == 2) {
+                bf8 fh[KB], fl[KB], gh[KB], gl[KB];
+                to_frags<HT, SPLIT>(h0, fh, fl);
+                to_frags<HT, SPLIT>(h1, gh, gl);
+                f16v acc1[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = zero;
+                gemm_bf<TT, KB, TT, SPLIT, IMG>(smem4, 1, 0, lane, acc1, fh, fl);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
+                f16v arz[2 * HT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
+                gemm_bf<TT, KB, 2 * HT, SPLIT, IMG>(smem4, 2, 0, lane, arz, gh, gl);
+                f16v ahn[HT];
+#pragma unroll
+                for (int j = 0; j < HT; ++j) ahn[j] = zero;
+                gemm_bf<TT, KB, HT, SPLIT, IMG>(smem4, 2, 2 * HT, lane, ahn, gh, gl);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
+                    gru_update_fast(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
+                }
+            }
+            float part = 0.0f;
+#pragma unroll
+            for (int t = 0; t < HT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    part += smem[G::OFF_WL + (half * HT + t) * 16 + i] * (L == 2 ? h1[t][i] : h0[t][i]);
+            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+            float d;
+            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+            if (half == 0 && valid) {
+                a.decoded[cw * N + jj] = d;
+                if (a.logits) a.logits[cw * N + ii] = out;
+            }
+            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+        }
+    }
+}
+
+static uint16_t bf16_rne(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+static float bf16_to_f(uint16_t b) {
+    uint32_t u = (uint32_t)b << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+// img: fp32 image of GeoB (bf16 fragments stored as raw bytes inside the float array)
+template <int F, int L, int SPLIT>
+static void build_image_bf(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
+                           float& b_lin, int64_t& wy_lo) {
+    using GB = GeoB<F, L, SPLIT>;
+    using G32 = Geo<F, L>;
+    constexpr int TT = GB::TT, HT = GB::HT, KB = GB::KB;
+    // reuse the fp32 builder for the extra / input / linear constants
+    std::vector<float> img32, wy32;
+    build_image<F, L>(W, N, onehot, img32, wy32, b_lin);
+    img.assign(GB::TOTAL, 0.0f);
+    const int Din = N + (onehot ? 2 : 1);
+    const float* p = W;
+    const float* wih[2];
+    const float* whh[2];
+    for (int l = 0; l < L; ++l) {
+        const int din = l == 0 ? Din : F;
+        wih[l] = p; p += (size_t)3 * F * din;
+        whh[l] = p; p += (size_t)3 * F * F;
+        p += 6 * F;
+    }
+    const float* mats[3] = {whh[0], L == 2 ? wih[1] : nullptr, L == 2 ? whh[1] : nullptr};
+    uint16_t* u16 = reinterpret_cast<uint16_t*>(img.data());
+    for (int g = 0; g < GB::NG; ++g)
+        for (int t = 0; t < TT; ++t)
+            for (int q = 0; q < KB; ++q)
+                for (int l = 0; l < 64; ++l)
+                    for (int j = 0; j < 8; ++j) {
+                        const int row = 32 * t + (l & 31), hh = l >> 5;
+                        const int th = q >> 1, s = q & 1;
+                        const int colk = 32 * th + 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
+                        const float v = mats[g][(size_t)row * F + colk];
+                        const uint16_t hi = bf16_rne(v);
+                        const size_t e = ((((size_t)(g * TT + t) * KB + q) * 64 + l) * 8 + j);
+                        u16[e] = hi;
+                        if (SPLIT == 3) u16[(size_t)GB::IMG * 2 + e] = bf16_rne(v - bf16_to_f(hi));
+                    }
+    for (int i = 0; i < GB::NG * TT * 64; ++i) img[GB::OFF_X + i] = img32[G32::OFF_X + i];
+    for (int i = 0; i < HT * 64; ++i) img[GB::OFF_IN + i] = img32[G32::OFF_IN + i];
+    for (int i = 0; i < 2 * HT * 16; ++i) img[GB::OFF_WL + i] = img32[G32::OFF_WL + i];
+    // y projection fragments: k-step q pairs lanes' y[16q + 8h + j]
+    const int nq = N / 16;
+    const size_t per = (size_t)TT * nq * 64 * 8;  // bf16 elements per image
+    wy.assign((per * (SPLIT == 3 ? 2 : 1) + 1) / 2, 0.0f);
+    uint16_t* w16 = reinterpret_cast<uint16_t*>(wy.data());
+    for (int t = 0; t < TT; ++t)
+        for (int q = 0; q < nq; ++q)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                    const int row = 32 * t + (l & 31);
+                    const int k = 16 * q + 8 * (l >> 5) + j;
+                    const float v = wih[0][(size_t)row * Din + k];
+                    const size_t e = (((size_t)t * nq + q) * 64 + l) * 8 + j;
+                    const uint16_t hi = bf16_rne(v);
+                    w16[e] = hi;
+                    if (SPLIT == 3) w16[per + e] = bf16_rne(v - bf16_to_f(hi));
+                }
+    wy_lo = (int64_t)(per / 8);  // in 16-B fragments
+}
+
+template <int F, int L, int SPLIT>
+static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
+    using G = GeoB<F, L, SPLIT>;
+    auto kern = gru_decode_bf_kernel<F, L, SPLIT>;
+    const size_t lds = (size_t)G::TOTAL * 4;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    const int64_t tiles = (a.B + 31) / 32;
+    const int64_t wgs = (tiles + 3) / 4;
+    const int grid = grid_for(wgs, 1, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+    (void)g;
+    return launch_check("gru_decode_bf_kernel launch");
+}
+
 }  // namespace gru
 }  // namespace npd
 
@@ -350,7 +665,8 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     NPD_ARG(N >= 8 && N <= kMaxN && N % 8 == 0, "npd_gru_create: N must be a multiple of 8 in [8, 256]");
     NPD_ARG(F == 32 || F == 64, "npd_gru_create: hidden size F must be 32 or 64 in this build");
     NPD_ARG(layers == 1 || layers == 2, "npd_gru_create: 1 or 2 GRU layers supported");
-    NPD_ARG(precision == 0, "npd_gru_create: only fp32 (precision 0) is built");
+    NPD_ARG(precision >= 0 && precision <= 2, "npd_gru_create: precision must be 0 (fp32), 1 (bf16x3) or 2 (bf16)");
+    NPD_ARG(precision == 0 || N % 16 == 0, "npd_gru_create: bf16 paths need N % 16 == 0");
     const int Din = N + (onehot ? 2 : 1);
     int64_t expect = (int64_t)3 * F * Din + (int64_t)3 * F * F + 6 * F;
     if (layers == 2) expect += (int64_t)6 * F * F + 6 * F;
@@ -358,15 +674,24 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     NPD_ARG(n_weights == expect, "npd_gru_create: weight count does not match (N, F, layers, onehot)");
     std::vector<float> img, wy;
     float b_lin = 0.0f;
-    if (F == 64 && layers == 2) gru::build_image<64, 2>(weights, N, onehot, img, wy, b_lin);
-    else if (F == 64) gru::build_image<64, 1>(weights, N, onehot, img, wy, b_lin);
-    else if (layers == 2) gru::build_image<32, 2>(weights, N, onehot, img, wy, b_lin);
-    else gru::build_image<32, 1>(weights, N, onehot, img, wy, b_lin);
+    int64_t wy_lo = 0;
+#define NPD_BUILD(FF, LL)                                                                              \
+    do {                                                                                               \
+        if (precision == 0) gru::build_image<FF, LL>(weights, N, onehot, img, wy, b_lin);              \
+        else if (precision == 1) gru::build_image_bf<FF, LL, 3>(weights, N, onehot, img, wy, b_lin, wy_lo); \
+        else gru::build_image_bf<FF, LL, 1>(weights, N, onehot, img, wy, b_lin, wy_lo);               \
+    } while (0)
+    if (F == 64 && layers == 2) NPD_BUILD(64, 2);
+    else if (F == 64) NPD_BUILD(64, 1);
+    else if (layers == 2) NPD_BUILD(32, 2);
+    else NPD_BUILD(32, 1);
+#undef NPD_BUILD
     npd_gru* g = new (std::nothrow) npd_gru;
     if (!g) return fail(NPD_ENOMEM, "npd_gru_create: out of memory");
     memset(g, 0, sizeof(*g));
     g->N = N; g->F = F; g->layers = layers; g->onehot = onehot; g->precision = precision; g->b_lin = b_lin;
     g->img_floats = (int64_t)img.size();
+    g->wy_lo = wy_lo;
     hipError_t e = hipGetDevice(&g->device);
     if (e == hipSuccess) e = hipMalloc(&g->img, img.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&g->wy, wy.size() * 4);
@@ -413,6 +738,21 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
     for (int i = 0; i < g->N; ++i)
         if (is_info[i]) a.info[i >> 5] |= 1u << (i & 31);
     hipStream_t s = (hipStream_t)stream;
+    if (g->precision != 0) {
+        gru::ArgsB b{};
+        b.img = g->img;
+        b.wy = reinterpret_cast<const gru::f4*>(g->wy);
+        b.y = y; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
+        b.rev = a.rev; b.onehot = a.onehot; b.b_lin = g->b_lin; b.wy_lo = g->wy_lo;
+        for (int w = 0; w < kMaxWords; ++w) b.info[w] = a.info[w];
+#define NPD_LBF(FF, LL) \
+        return g->precision == 1 ? gru::launch_bf<FF, LL, 3>(g, b, s) : gru::launch_bf<FF, LL, 1>(g, b, s)
+        if (g->F == 64 && g->layers == 2) NPD_LBF(64, 2);
+        if (g->F == 64) NPD_LBF(64, 1);
+        if (g->layers == 2) NPD_LBF(32, 2);
+        NPD_LBF(32, 1);
+#undef NPD_LBF
+    }
     if (g->F == 64 && g->layers == 2) return gru::launch<64, 2>(g, a, s);
     if (g->F == 64) return gru::launch<64, 1>(g, a, s);
     if (g->layers == 2) return gru::launch<32, 2>(g, a, s);

@@ -95,9 +95,17 @@ class _GruHandle:
 
 class RNN_decoder:
     """rnn_all.RNN_decoder (rnn_all.py:400-561): eval (``train=False``) decoding for decoding_type
-    'y_input' runs fused on the GPU."""
+    'y_input' runs fused on the GPU.
 
-    def __init__(self, decoding_type, N, info_inds, onehot=False, reverse_order=False):
+    ``precision`` (keyword, not in the reference): "fp32" (default; the reference's arithmetic),
+    "bf16x3" (split-bf16 MFMA, ~fp32 accuracy) or "bf16" (plain bf16 MFMA, fp32 accumulation)."""
+
+    PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16": 2}
+
+    def __init__(self, decoding_type, N, info_inds, onehot=False, reverse_order=False, precision="fp32"):
+        if precision not in self.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(self.PRECISIONS)}")
+        self.precision = precision
         self.decoding_type = decoding_type
         self.N = N
         self.info_inds = info_inds
@@ -107,14 +115,15 @@ class RNN_decoder:
 
     def _handle(self, net: RNN_Model, device):
         # re-pack when the weights change (parameter versions) or the device differs
-        key = (id(net), str(device), tuple(p._version for p in net.parameters()),
+        key = (id(net), str(device), self.precision, tuple(p._version for p in net.parameters()),
                tuple(p.data_ptr() for p in net.parameters()))
         h = self._cache.get(key)
         if h is None:
             self._cache.clear()
             W = pack_gru_weights(net, net.num_rnn_layers)
             with torch.cuda.device(device):
-                h = _GruHandle(self.N, net.feature_size, net.num_rnn_layers, self.onehot, W)
+                h = _GruHandle(self.N, net.feature_size, net.num_rnn_layers, self.onehot, W,
+                               self.PRECISIONS[self.precision])
             self._cache[key] = h
         return h
 
