@@ -20,6 +20,7 @@ oracle: $(ORACLE)
 # per-file extras: the SC kernel never sees NaN (finite LLRs), so fmin needs no canonicalisation
 EXTRA_npd_sc := -fno-honor-nans
 EXTRA_npd_sc_fast := -fno-honor-nans
+EXTRA_npd_scl := -fno-honor-nans
 
 $(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(CHDR)
 	@mkdir -p $(OBJDIR)
@@ -29,8 +30,12 @@ $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,--no-undefined
 
 # Oracle: plain C, no fast-math, no FMA contraction (exact restatement of the reference's fp32 ops).
-$(ORACLE): oracle/npd_oracle.c
-	gcc -O2 -std=c11 -fPIC -shared -fopenmp -ffp-contract=off -o $@ $< -lm
+# The SCL restatement is C++ so that list pruning calls libstdc++'s std::nth_element (torch.topk's CPU path).
+$(ORACLE): oracle/npd_oracle.c oracle/npd_oracle_scl.cpp
+	@mkdir -p build/oracle
+	gcc -O2 -std=c11 -fPIC -fopenmp -ffp-contract=off -c oracle/npd_oracle.c -o build/oracle/npd_oracle.o
+	g++ -O2 -std=c++17 -fPIC -fopenmp -ffp-contract=off -c oracle/npd_oracle_scl.cpp -o build/oracle/npd_oracle_scl.o
+	g++ -shared -fopenmp -o $@ build/oracle/npd_oracle.o build/oracle/npd_oracle_scl.o -lm
 
 asm: $(CSRC)
 	@mkdir -p build/asm

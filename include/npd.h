@@ -107,6 +107,31 @@ int npd_sc_decode(const npd_code* code, const float* y, float llr_scale, float* 
 int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_scale, float* msg_hat, uint64_t seed,
                      uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream);
 
+/* ---------------------------------------------------------------------------------- SC-List decode */
+/*
+ * Successive-cancellation list decoding, PolarCode.scl_decode(y, snr, L, use_CRC=False)
+ * (polar.py:793-876) with pruneLists (polar.py:777-791): min-sum SC per path (no frozen prior in the
+ * LLRs), path metric += |leaf| on a frozen leaf with sign(leaf) != 1 and on the flipped branch of an
+ * information leaf; survivors = torch.topk's choice (ties resolved exactly as std::nth_element, see
+ * npd_list_prune_select) in list order; final path = the first minimum of ||encode(u) - y||^2.
+ * Polar codes, 8 <= N <= 64, 1 <= list_size <= 8, y 16-byte aligned.  Outputs: msg_hat (B,K) and
+ * u_hat (B,N) of the chosen path, each optional.  scl_decode's leaf-LLR output equals
+ * npd_sc_decode(..., gt = u_hat) (a genie pass reproduces the chosen path's LLRs bit for bit).
+ * Decisions are bit-exact with the reference except when two list candidates' fp32 distances differ
+ * only by summation order (torch's vectorised sum vs a sequential one here).
+ */
+int npd_scl_decode(const npd_code* code, const float* y, float llr_scale, int list_size, float* msg_hat,
+                   float* u_hat, int64_t B, void* stream);
+/* Monte-Carlo SC-List decode with fused error counting (semantics of npd_sc_decode_mc). */
+int npd_scl_decode_mc(const npd_code* code, const float* y, float llr_scale, int list_size, float* msg_hat,
+                      uint64_t seed, uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream);
+/*
+ * Host utility (no GPU): the survivor set of pruneLists for n <= 16 candidates whose negated metrics
+ * are neg_metrics[0..n) in list order, keeping `keep` -- bit c of *mask_out set iff candidate c
+ * survives.  The same code runs inside the SCL kernel when metrics tie across the boundary.
+ */
+int npd_list_prune_select(const float* neg_metrics, int n, int keep, uint32_t* mask_out);
+
 /* ---------------------------------------------------------------------------------- counters */
 /*
  * counters[0] += #(round(ref) != round(hat)), counters[1] += #rows with any such element, over

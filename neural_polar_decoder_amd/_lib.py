@@ -33,6 +33,10 @@ SIGNATURES = [
                                 c_void_p]),
     ("npd_sc_decode", c_int, [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     ("npd_sc_decode_mc", c_int, [c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_i64, c_void_p, c_void_p]),
+    ("npd_scl_decode", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p, c_i64, c_void_p]),
+    ("npd_scl_decode_mc", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_u64, c_u64, c_i64, c_void_p,
+                                  c_void_p]),
+    ("npd_list_prune_select", c_int, [c_void_p, c_int, c_int, c_void_p]),
     ("npd_count_errors", c_int, [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p]),
     ("npd_gru_create", c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
     ("npd_gru_destroy", c_int, [c_void_p]),

@@ -1,0 +1,500 @@
+// npd_scl.hip -- Polar SC-List decoding (PolarCode.scl_decode, polar.py:793-876, use_CRC=False).
+//
+// Layout: a list of L paths per codeword lives in G = pow2ceil(L) adjacent lanes, one path per lane,
+// so 64/G codewords share a wave.  Every lane runs the same compile-time-unrolled min-sum SC schedule
+// as npd_sc_fast.hip on its own path state (LLRs of each level and partial sums in VGPRs); the
+// channel LLRs are identical for the whole group and never move.
+//
+// At an information leaf the group's 2s candidates (s = current list size) are, in the reference's
+// list order, [keep_0 .. keep_{s-1}, flip_0 .. flip_{s-1}] with metrics m_j and fl32(m_j + |l_j|)
+// (polar.py:830-843).  When 2s > L the survivors are torch.topk's choice (polar.py:777-791): if no
+// metric tie straddles the L-th place the survivor set is unique and is found by rank counting (two
+// ballots); otherwise the group runs the exact std::nth_element statement of npd_nth.hpp.  Survivors
+// keep list order.  Lane j then takes its candidate's parent state through ds_bpermute -- only the
+// values that are still live after this leaf (known at compile time from the leaf index), never the
+// channel level.
+//
+// The final choice is the reference's ML step (polar.py:868-874): each path's codeword
+// (encode_plotkin of its decisions, computed on sign/zero bit masks) is compared with y in fp32 and the
+// first minimum wins.  The leaf LLRs of the chosen path (scl_decode's first output) equal a genie SC
+// pass with gt = the chosen u_hat; the host wrapper runs npd_sc_decode for that when asked.
+#include "npd_common.hpp"
+#include "npd_nth.hpp"
+
+namespace npd {
+namespace scl {
+
+struct Args {
+    const float* y;
+    float* msg;                    // (B,K) or null
+    float* uhat;                   // (B,N) or null
+    unsigned long long* counters;  // {bit errors, block errors} or null
+    uint64_t seed;
+    uint64_t cw_offset;
+    int64_t B;
+    int64_t ntiles;
+    float scale;
+    int L;
+    uint32_t count;
+};
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+constexpr int log2c() {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    return n;
+}
+
+template <int C>
+__device__ __forceinline__ int swz(int r) {
+    if constexpr (C >= 16) return r & 15;
+    else return (r / (16 / C)) % C;
+}
+
+__device__ __forceinline__ float rmul(float a, float b) {
+    float r = a * b;
+    asm("" : "+v"(r));  // keep the product rounded (no fma contraction into a following add)
+    return r;
+}
+
+__device__ __forceinline__ float f_minsum(float a, float b) {
+    const float m = __builtin_fminf(__builtin_fabsf(a), __builtin_fabsf(b));
+    return bitsf(fbits(m) | ((fbits(a) ^ fbits(b)) & 0x80000000u));
+}
+
+__device__ __forceinline__ float sgn_bits(float x) {
+    const float s = bitsf((fbits(x) & 0x80000000u) | 0x3f800000u);
+    return (x == 0.0f) ? 0.0f : s;
+}
+
+// value of lane (group base + T) for every lane of a G-lane group
+template <int G, int T>
+__device__ __forceinline__ float gb(float x, int src_lane) {
+    if constexpr (G == 1) {
+        return x;
+    } else if constexpr (G == 2) {
+        constexpr int ctl = T | (T << 2) | ((2 + T) << 4) | ((2 + T) << 6);
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), ctl, 0xF, 0xF, false));
+    } else if constexpr (G == 4) {
+        constexpr int ctl = T * 0x55;
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), ctl, 0xF, 0xF, false));
+    } else {
+        return __shfl(x, src_lane, 64);
+    }
+}
+
+template <int N, int G>
+struct Lane {
+    static constexpr int W = (N + 31) / 32;
+    float lv[2 * N];   // level d at lv[2^d .. 2^(d+1)); channel level at lv[N .. 2N)
+    float beta[N];     // partial sums
+    float m;           // path metric (polar.py:803)
+    uint32_t sm[W];    // decision sign bits by position (u = -1)
+    uint32_t zm[W];    // decision zero bits by position (u = 0, from sign(0))
+    uint32_t fz[W];    // frozen bits (re-materialised per tile)
+    int base;          // lane id of the group's first lane
+    int j;             // index within the group (= list slot)
+    uint32_t slot;     // wave-uniform: information bits decided so far
+    int L;
+};
+
+// first position whose partial sum is still read after leaf I: the start of the highest ancestor that
+// still needs its left block for a g-update, or that will combine partial sums (spine nodes skip it)
+template <int N, int I>
+constexpr int beta_live_start() {
+    constexpr int n = log2c<N>();
+    for (int D = n; D >= 1; --D) {
+        const int S0 = (I >> D) << D;
+        const int h = 1 << (D - 1);
+        const bool inleft = (I - S0) < h;
+        const bool spine = S0 + (1 << D) == N;
+        if (inleft || !spine) return S0;
+    }
+    return I;
+}
+
+template <int N, int G, int I, int D>
+__device__ __forceinline__ void copy_levels(Lane<N, G>& c, int src) {
+    if constexpr (D >= 1) {
+        if constexpr (((I >> (D - 1)) & 1) == 0) {  // I in the left child of its level-D ancestor: input live
+#pragma unroll
+            for (int k = (1 << D); k < (2 << D); ++k) c.lv[k] = __shfl(c.lv[k], src, 64);
+        }
+        copy_levels<N, G, I, D - 1>(c, src);
+    }
+}
+
+template <int N, int G, int I>
+__device__ __forceinline__ void copy_live(Lane<N, G>& c, int src) {
+    constexpr int n = log2c<N>();
+    copy_levels<N, G, I, n - 1>(c, src);
+    constexpr int b0 = beta_live_start<N, I>();
+#pragma unroll
+    for (int k = b0; k < I; ++k) c.beta[k] = __shfl(c.beta[k], src, 64);
+#pragma unroll
+    for (int w = 0; w <= (I >> 5); ++w) {
+        c.sm[w] = (uint32_t)__shfl((int)c.sm[w], src, 64);
+        c.zm[w] = (uint32_t)__shfl((int)c.zm[w], src, 64);
+    }
+}
+
+// survivors of pruneLists for one group when a metric tie straddles the L-th place (rare): exact rule
+template <int G>
+__device__ __noinline__ uint32_t exact_mask(const float (&km)[G], const float (&fm)[G], int s, int L) {
+    float negm[16];
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+        negm[t] = -1.0f * km[t];
+        negm[G + t] = -1.0f * fm[t];
+    }
+    // list order is [keep_0..keep_{s-1}, flip_0..flip_{s-1}]: compact when s < G
+    float v[16];
+    for (int c2 = 0; c2 < s; ++c2) {
+        v[c2] = negm[c2];
+        v[s + c2] = negm[G + c2];
+    }
+    return nth::prune_mask(v, 2 * s, L);
+}
+
+template <int N, int G, int I>
+__device__ __forceinline__ void info_leaf(Lane<N, G>& c, float l, int lane) {
+    const float a = __builtin_fabsf(l);
+    const int L = c.L;
+    const uint32_t slot = c.slot;
+    const int s = slot >= 3u ? L : ((1 << slot) < L ? (1 << slot) : L);
+    const bool prune = 2 * s > L;
+    uint32_t msel;
+    if (prune) {
+        float km[G], fm[G];
+        const int bl = c.base;
+        km[0] = gb<G, 0>(c.m, bl + 0);
+        fm[0] = km[0] + gb<G, 0>(a, bl + 0);
+        if constexpr (G > 1) {
+            km[1] = gb<G, 1>(c.m, bl + 1);
+            fm[1] = km[1] + gb<G, 1>(a, bl + 1);
+        }
+        if constexpr (G > 2) {
+            km[2] = gb<G, 2>(c.m, bl + 2);
+            fm[2] = km[2] + gb<G, 2>(a, bl + 2);
+            km[3] = gb<G, 3>(c.m, bl + 3);
+            fm[3] = km[3] + gb<G, 3>(a, bl + 3);
+        }
+        if constexpr (G > 4) {
+#pragma unroll
+            for (int t = 4; t < G; ++t) {
+                km[t] = __shfl(c.m, bl + t, 64);
+                fm[t] = km[t] + __shfl(a, bl + t, 64);
+            }
+        }
+        const float vk = c.m, vf = c.m + a;
+        int ltk = 0, lek = 0, ltf = 0, lef = 0;
+#pragma unroll
+        for (int t = 0; t < G; ++t) {
+            if (t < s) {
+                ltk += (km[t] < vk) + (fm[t] < vk);
+                lek += (km[t] <= vk) + (fm[t] <= vk);
+                ltf += (km[t] < vf) + (fm[t] < vf);
+                lef += (km[t] <= vf) + (fm[t] <= vf);
+            }
+        }
+        const bool act = c.j < s;
+        const bool sk = act && ltk < L;
+        const bool sf = act && ltf < L;
+        const bool st = act && ((ltk < L && lek > L) || (ltf < L && lef > L));
+        const unsigned long long bk = __ballot(sk), bf = __ballot(sf), bs = __ballot(st);
+        const uint32_t lowm = (1u << s) - 1u;
+        msel = ((uint32_t)(bk >> bl) & lowm) | (((uint32_t)(bf >> bl) & lowm) << s);
+        if (bs) {
+            const bool mine = ((uint32_t)(bs >> bl) & ((G >= 32) ? 0xFFFFFFFFu : ((1u << G) - 1u))) != 0u;
+            if (mine) msel = exact_mask<G>(km, fm, s, L);
+        }
+    } else {
+        msel = (1u << (2 * s)) - 1u;
+    }
+    // list slot j takes the j-th surviving candidate (list order)
+    uint32_t mm = msel;
+#pragma unroll
+    for (int t = 0; t < G - 1; ++t)
+        if (t < c.j) mm &= mm - 1u;
+    const int cidx = mm ? __builtin_ctz(mm) : c.j;
+    const bool flip = mm ? (cidx >= s) : false;
+    const int srcj = flip ? cidx - s : (mm ? cidx : c.j);
+    float u;
+    if constexpr (G == 1) {
+        u = sgn_bits(l);
+        if (flip) {
+            u = -u;
+            c.m = c.m + a;
+        }
+    } else {
+        const int src = c.base + srcj;
+        const float ls = __shfl(l, src, 64);
+        const float ms = __shfl(c.m, src, 64);
+        copy_live<N, G, I>(c, src);
+        u = sgn_bits(ls);
+        if (flip) u = -u;
+        c.m = flip ? ms + __builtin_fabsf(ls) : ms;
+    }
+    c.beta[I] = u;
+    c.sm[I >> 5] |= (u < 0.0f ? 1u : 0u) << (I & 31);
+    c.zm[I >> 5] |= (u == 0.0f ? 1u : 0u) << (I & 31);
+    c.slot = slot + 1u;
+    (void)lane;
+}
+
+template <int N, int G, int I>
+__device__ __forceinline__ void leaf(Lane<N, G>& c, float l, int lane) {
+    const bool frozen = (c.fz[I >> 5] >> (I & 31)) & 1u;
+    if (frozen) {
+        const float pen = (l > 0.0f) ? 0.0f : __builtin_fabsf(l);  // |l| * (sign(l) != 1), polar.py:814
+        c.m = c.m + pen;
+        c.beta[I] = 1.0f;
+    } else {
+        info_leaf<N, G, I>(c, l, lane);
+    }
+}
+
+template <int N, int G, int D, int S0>
+__device__ __forceinline__ void node(Lane<N, G>& c, int lane) {
+    if constexpr (D == 0) {
+        leaf<N, G, S0>(c, c.lv[1], lane);
+    } else {
+        constexpr int h = 1 << (D - 1);
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
+        node<N, G, D - 1, S0>(c, lane);
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[S0 + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+        node<N, G, D - 1, S0 + h>(c, lane);
+        if constexpr (S0 + (1 << D) < N) {  // nodes on the right spine never feed a g-update
+#pragma unroll
+            for (int j = 0; j < h; ++j) c.beta[S0 + j] = c.beta[S0 + j] * c.beta[S0 + h + j];
+        }
+    }
+}
+
+template <int N, int G>
+__global__ __launch_bounds__(64) void scl_kernel(const CodeParams p, const Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int n = log2c<N>();
+    constexpr int C = N / 4;      // 16-B chunks per row
+    constexpr int T = 64 / G;     // codewords per wave tile
+    constexpr int W = (N + 31) / 32;
+    const int lane = threadIdx.x;
+    const f4* y4 = reinterpret_cast<const f4*>(a.y);
+    const int64_t last4 = a.B * C - 1;
+    const int K = p.K;
+
+    Lane<N, G> c;
+    c.j = lane & (G - 1);
+    c.base = lane - c.j;
+    c.L = a.L;
+    const int r = lane / G;       // row of this lane's codeword in the tile
+    const int sw = swz<C>(r);
+    const int s_final = K >= 3 ? a.L : ((1 << K) < a.L ? (1 << K) : a.L);
+
+    uint32_t err_bits = 0, err_blocks = 0;
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t row0 = t * T;
+        // ---- stage the tile's received words in LDS (coalesced), swizzled rows
+        __syncthreads();
+        for (int i = lane; i < T * C; i += 64) {
+            const int rr = i / C, cc = i % C;
+            int64_t gi = row0 * C + i;
+            gi = gi < last4 ? gi : last4;
+            *reinterpret_cast<f4*>(lds + 16 * (rr * C + (cc ^ swz<C>(rr)))) = y4[gi];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const f4 v = *reinterpret_cast<const f4*>(lds + 16 * (r * C + (q ^ sw)));
+            c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
+            c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
+            c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
+            c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            uint32_t fw = p.frozen[w];
+            asm volatile("" : "+s"(fw));
+            c.fz[w] = fw;
+            c.sm[w] = 0u;
+            c.zm[w] = 0u;
+        }
+        c.m = 0.0f;
+        c.slot = 0u;
+        node<N, G, n, 0>(c, lane);
+
+        // ---- ML choice (polar.py:868-874): codeword of each path from its decision bits
+        uint32_t S[W], Z[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            S[w] = c.sm[w];
+            Z[w] = c.zm[w];
+        }
+        constexpr uint32_t kLow[5] = {0x55555555u, 0x33333333u, 0x0F0F0F0Fu, 0x00FF00FFu, 0x0000FFFFu};
+#pragma unroll
+        for (int d = 0; d < (n < 5 ? n : 5); ++d) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                S[w] ^= (S[w] >> (1 << d)) & kLow[d];
+                Z[w] |= (Z[w] >> (1 << d)) & kLow[d];
+            }
+        }
+        if constexpr (n == 6) {
+            S[0] ^= S[1];
+            Z[0] |= Z[1];
+        }
+        float dist = 0.0f;
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const f4 v = *reinterpret_cast<const f4*>(lds + 16 * (r * C + (q ^ sw)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = 4 * q + e;
+                const uint32_t sb = (S[k >> 5] >> (k & 31)) & 1u, zb = (Z[k >> 5] >> (k & 31)) & 1u;
+                const float cv = zb ? 0.0f : (sb ? -1.0f : 1.0f);
+                const float dd = cv - v[e];
+                dist = dist + rmul(dd, dd);
+            }
+        }
+        float bd = c.j < s_final ? dist : __builtin_inff();
+        int bi = c.j;
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const float od = __shfl_xor(bd, off, 64);
+            const int oi = __shfl_xor(bi, off, 64);
+            if (od < bd || (od == bd && oi < bi)) {
+                bd = od;
+                bi = oi;
+            }
+        }
+        const int64_t cw = row0 + r;
+        if (c.j == bi && cw < a.B) {
+            uint32_t e = 0;
+            uint32_t mw[4] = {0u, 0u, 0u, 0u};
+            if (a.count) {
+                const u32x4 o = philox_block(a.seed, kStreamMsg, a.cw_offset + (uint64_t)cw, 0u);
+                mw[0] = o.x;
+                mw[1] = o.y;
+                mw[2] = o.z;
+                mw[3] = o.w;
+            }
+            float* mrow = a.msg ? a.msg + cw * K : nullptr;
+            for (int k = 0; k < K; ++k) {
+                const int pos = p.info[k];
+                const uint32_t sw0 = W > 1 && pos >= 32 ? c.sm[W - 1] : c.sm[0];
+                const uint32_t zw0 = W > 1 && pos >= 32 ? c.zm[W - 1] : c.zm[0];
+                const uint32_t sb = (sw0 >> (pos & 31)) & 1u, zb = (zw0 >> (pos & 31)) & 1u;
+                if (mrow) mrow[k] = zb ? 0.0f : (sb ? -1.0f : 1.0f);
+                e += ((sb ^ ((mw[k >> 5] >> (k & 31)) & 1u)) | zb);
+            }
+            if (a.uhat) {
+                float* urow = a.uhat + cw * N;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    const uint32_t sb = (c.sm[k >> 5] >> (k & 31)) & 1u, zb = (c.zm[k >> 5] >> (k & 31)) & 1u;
+                    urow[k] = zb ? 0.0f : (sb ? -1.0f : 1.0f);
+                }
+            }
+            err_bits += e;
+            err_blocks += e ? 1u : 0u;
+        }
+    }
+    if (a.count) {
+        const uint32_t eb = wave_sum_u32(err_bits);
+        const uint32_t bl = wave_sum_u32(err_blocks);
+        if (lane == 0) {
+            atomicAdd(a.counters + 0, (unsigned long long)eb);
+            atomicAdd(a.counters + 1, (unsigned long long)bl);
+        }
+    }
+}
+
+template <int N, int G>
+static int launch(const CodeParams& p, Args a, hipStream_t s) {
+    constexpr int T = 64 / G;
+    const size_t lds = (size_t)T * N * 4;
+    a.ntiles = (a.B + T - 1) / T;
+    auto kern = scl_kernel<N, G>;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, p, a);
+    return launch_check("scl_kernel launch");
+}
+
+template <int N>
+static int launch_n(const CodeParams& p, const Args& a, hipStream_t s) {
+    if (a.L == 1) return launch<N, 1>(p, a, s);
+    if (a.L == 2) return launch<N, 2>(p, a, s);
+    if (a.L <= 4) return launch<N, 4>(p, a, s);
+    return launch<N, 8>(p, a, s);
+}
+
+static int run(const npd_code* code, Args& a, hipStream_t s) {
+    const CodeParams& p = code->p;
+    if (p.pac) return fail(NPD_ENOTSUP, "scl_decode: the reference defines SC-List for Polar codes only");
+    if (p.N < 8 || p.N > 64) return fail(NPD_ENOTSUP, "scl_decode: N must be 8..64 in this build");
+    if (a.L < 1 || a.L > 8) return fail(NPD_EINVAL, "scl_decode: list size must be 1..8");
+    if ((((uintptr_t)a.y) & 15) != 0) return fail(NPD_EINVAL, "scl_decode: y must be 16-byte aligned");
+    if (a.B == 0) return NPD_OK;
+    switch (p.N) {
+        case 8: return launch_n<8>(p, a, s);
+        case 16: return launch_n<16>(p, a, s);
+        case 32: return launch_n<32>(p, a, s);
+        default: return launch_n<64>(p, a, s);
+    }
+}
+
+}  // namespace scl
+}  // namespace npd
+
+using namespace npd;
+
+extern "C" int npd_scl_decode(const npd_code* code, const float* y, float llr_scale, int list_size, float* msg_hat,
+                              float* u_hat, int64_t B, void* stream) {
+    NPD_ARG(code != nullptr, "npd_scl_decode: code is NULL");
+    NPD_ARG(B >= 0, "npd_scl_decode: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_scl_decode: y is NULL");
+    scl::Args a{};
+    a.y = y;
+    a.msg = msg_hat;
+    a.uhat = u_hat;
+    a.B = B;
+    a.scale = llr_scale;
+    a.L = list_size;
+    return scl::run(code, a, (hipStream_t)stream);
+}
+
+extern "C" int npd_scl_decode_mc(const npd_code* code, const float* y, float llr_scale, int list_size,
+                                 float* msg_hat, uint64_t seed, uint64_t cw_offset, int64_t B,
+                                 unsigned long long* counters, void* stream) {
+    NPD_ARG(code != nullptr, "npd_scl_decode_mc: code is NULL");
+    NPD_ARG(B >= 0, "npd_scl_decode_mc: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_scl_decode_mc: y is NULL");
+    NPD_ARG(counters != nullptr, "npd_scl_decode_mc: counters is NULL");
+    scl::Args a{};
+    a.y = y;
+    a.msg = msg_hat;
+    a.counters = counters;
+    a.seed = seed;
+    a.cw_offset = cw_offset;
+    a.B = B;
+    a.scale = llr_scale;
+    a.L = list_size;
+    a.count = 1u;
+    return scl::run(code, a, (hipStream_t)stream);
+}
+
+extern "C" int npd_list_prune_select(const float* neg_metrics, int n, int keep, uint32_t* mask_out) {
+    NPD_ARG(neg_metrics != nullptr && mask_out != nullptr, "npd_list_prune_select: NULL pointer");
+    NPD_ARG(n >= 1 && n <= 16 && keep >= 1 && keep <= n, "npd_list_prune_select: need 1 <= keep <= n <= 16");
+    *mask_out = nth::prune_mask(neg_metrics, n, keep);
+    return NPD_OK;
+}

@@ -163,6 +163,38 @@ class PolarCode:
                                              y.shape[0], _lib.stream_of(y.device)), "npd_sc_decode")
         return hat
 
+    # ------------------------------------------------------------------ SC-List (polar.py:793-876)
+    def scl_decode(self, corrupted_codewords, snr, L=1, use_CRC=False, want_llrs=True):
+        """SC-List decoding; returns (leaf LLRs of the chosen path (B,N), msg_hat (B,K)).
+
+        The chosen path's leaf LLRs are recomputed by a genie SC pass with its decisions (identical
+        values); ``want_llrs=False`` skips that pass and returns None in their place."""
+        if use_CRC:
+            raise NotImplementedError("scl_decode(use_CRC=True) depends on module globals of the reference "
+                                      "(polar.py:741-763: `polar.CRC_len`); only the use_CRC=False path is built")
+        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
+        y = _aligned(_lib.f32c(corrupted_codewords))
+        B = y.shape[0]
+        hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
+        uh = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if want_llrs else None
+        st = _lib.stream_of(y.device)
+        _lib.check(_lib.load().npd_scl_decode(self.code.h, _lib.ptr(y), llr_scale(snr), int(L), _lib.ptr(hat),
+                                              _lib.ptr(uh), B, st), "npd_scl_decode")
+        if not want_llrs:
+            return None, hat
+        leaf = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
+        _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(leaf), None, None,
+                                             _lib.ptr(uh), B, st), "npd_sc_decode (genie leaf LLRs)")
+        return leaf, hat
+
+    def scl_decode_mc(self, y, snr, L, seed, cw_offset, counters, msg_hat=None):
+        _lib.require_gpu(y, "y")
+        y = _aligned(y)
+        _lib.check(_lib.load().npd_scl_decode_mc(self.code.h, _lib.ptr(y), llr_scale(snr), int(L), _lib.ptr(msg_hat),
+                                                 int(seed), int(cw_offset), y.shape[0], _lib.ptr(counters),
+                                                 _lib.stream_of(y.device)), "npd_scl_decode_mc")
+        return counters
+
     # The reference's ``sc_decode`` (polar.py:209-279) is a different (exact-LSE, soft) decoder that
     # the eval loops do not call; out of scope here (SURVEY.md sec. 8(f)).
 
@@ -183,6 +215,11 @@ class PolarCode:
                                                 int(cw_offset), y.shape[0], _lib.ptr(counters), _lib.stream_of(y.device)),
                    "npd_sc_decode_mc")
         return counters
+
+
+def _aligned(y: torch.Tensor) -> torch.Tensor:
+    """The list kernel reads 16-byte vectors: re-base an unaligned view (rare: odd row offsets)."""
+    return y if y.data_ptr() % 16 == 0 else y.clone()
 
 
 def reference_polar_code(N: int, K: int, args=None, infty=1000.) -> PolarCode:

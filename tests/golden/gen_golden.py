@@ -7,6 +7,7 @@ Run in the build container only (``/root/reference`` does not exist on the GPU b
 
 Every fixture is data: inputs and the reference's outputs for them.  Reference functions called:
   PolarCode.__init__ / encode_plotkin / channel / sc_decode_new       polar.py:66-148, 201-207, 465-484
+  PolarCode.scl_decode (use_CRC=False)                                polar.py:777-876
   PAC.__init__ / pac_encode / pac_sc_decode                           pac_code.py:97-224, 534-573
   rnn_all.get_code                                                    rnn_all.py:1015-1196
   RNN_Model / RNN_decoder.decode (test branch, y_input, onehot)       rnn_all.py:294-561
@@ -154,6 +155,34 @@ def gen_sc():
              gt_y=y.numpy(), gt=gt.numpy(), gt_snr=np.float64(1.0), gt_leaf=gleaf.numpy(), gt_msg_hat=ghat.numpy())
 
 
+def tie_rows(N, rng, count):
+    """Received words on a coarse grid: |LLR| values repeat, so list metrics tie at the pruning boundary
+    and exact zeros occur -- pins torch.topk's tie rule and sign(0) paths."""
+    grid = np.array([-1.5, -1.0, -0.5, 0.0, 0.5, 1.0, 1.5], np.float32)
+    return grid[rng.integers(0, grid.size, (count, N))]
+
+
+def gen_scl():
+    rng = np.random.default_rng(8)
+    for N, K, L, per in [(64, 32, 4, 48), (32, 16, 4, 64), (16, 8, 2, 64), (64, 32, 8, 24), (32, 16, 1, 64),
+                         (32, 16, 3, 48), (8, 4, 4, 64)]:
+        code = polar_code(N, K)
+        torch.manual_seed(2000 + N + K + L)
+        ys, snrs, leafs, hats = [], [], [], []
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (per, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            leaf, hat = code.scl_decode(y, float(snr), L, use_CRC=False)
+            ys.append(y.numpy()); snrs.append(np.full(per, snr)); leafs.append(leaf.numpy()); hats.append(hat.numpy())
+        for snr in (1.0, 3.0):
+            y = torch.from_numpy(np.concatenate([tie_rows(N, rng, per), crafted_rows(N, rng)]))
+            leaf, hat = code.scl_decode(y, snr, L, use_CRC=False)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); leafs.append(leaf.numpy())
+            hats.append(hat.numpy())
+        save(f"scl_{N}_{K}_L{L}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), leaf=np.concatenate(leafs),
+             msg_hat=np.concatenate(hats), info=np.asarray(code.info_positions, np.int64), L=np.int64(L))
+
+
 def gen_pac():
     rng = np.random.default_rng(6)
     for N, K, per in [(128, 64, 64), (64, 22, 96), (32, 16, 128)]:
@@ -272,6 +301,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "pac", "errors", "gru", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "pac", "errors", "gru", "conv"]
     for w in which:
         globals()["gen_" + w]()

@@ -79,3 +79,23 @@ def test_product_path_refuses_host_tensors():
     code = reference_polar_code(64, 32)
     with pytest.raises(NpdError):
         code.sc_decode_new(torch.zeros(4, 64), 1.0)
+
+
+def test_list_prune_select_host_utility_matches_std_nth_element(oracle):
+    """npd_list_prune_select (the tie rule compiled into the SCL kernel) == std::nth_element (oracle)."""
+    import ctypes
+    import numpy as np
+    from neural_polar_decoder_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(3)
+    m = ctypes.c_uint32()
+    for n in range(1, 17):
+        for k in range(1, n + 1):
+            for _ in range(60):
+                v = (-rng.integers(0, 3, n)).astype(np.float32)
+                assert L.npd_list_prune_select(v.ctypes.data_as(ctypes.c_void_p), n, k, ctypes.byref(m)) == 0
+                got = {i for i in range(n) if (m.value >> i) & 1}
+                assert got == set(oracle.topk_select(v, k).tolist()), (n, k, v)
+    assert L.npd_list_prune_select(None, 4, 2, ctypes.byref(m)) < 0
+    v = np.zeros(20, np.float32)
+    assert L.npd_list_prune_select(v.ctypes.data_as(ctypes.c_void_p), 20, 2, ctypes.byref(m)) < 0

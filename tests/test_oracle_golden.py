@@ -126,3 +126,31 @@ def test_oracle_mc_is_generate_then_decode(oracle):
         _, hat = oracle.sc_decode(y, snr, info)
         be, bl = oracle.count_errors(msg, hat)
         assert (be, bl) == oracle.mc_sc(B, N, info, snr, seed, si, cw_offset=4096)
+
+
+SCL_FIXTURES = ["scl_64_32_L4", "scl_32_16_L4", "scl_16_8_L2", "scl_64_32_L8", "scl_32_16_L1", "scl_32_16_L3",
+                "scl_8_4_L4"]
+
+
+@pytest.mark.parametrize("name", SCL_FIXTURES)
+def test_scl_oracle_golden(oracle, name):
+    """SC-List restatement == PolarCode.scl_decode bit for bit (msg_hat and chosen path's leaf LLRs),
+    including tie-heavy grid-valued received words and exact zeros."""
+    d = golden(f"{name}.npz")
+    for s in np.unique(d["snr"]):
+        m = d["snr"] == s
+        leaf, hat, _ = oracle.scl_decode(d["y"][m], float(s), d["info"], int(d["L"]))
+        assert np.array_equal(hat, d["msg_hat"][m]), (name, s)
+        assert np.array_equal(leaf, d["leaf"][m]), (name, s)
+
+
+def test_topk_tie_rule_matches_torch(oracle):
+    """pruneLists' survivor set == torch.topk(-metric, L, 0) on CPU, with heavy ties (the rule the SCL
+    kernel reproduces); the naive lowest-index rule would differ in ~40 % of these cases."""
+    import torch
+    rng = np.random.default_rng(0)
+    for n, k in [(2, 1), (4, 2), (6, 3), (8, 4), (16, 8), (8, 3), (4, 3), (16, 5), (12, 7), (10, 5)]:
+        v = (-rng.integers(0, 4, (400, n))).astype(np.float32)
+        tk = torch.topk(torch.from_numpy(v.T.copy()), k, 0).indices.T.numpy()
+        for row, t in zip(v, tk):
+            assert set(oracle.topk_select(row, k).tolist()) == set(t.tolist()), (n, k, row)
