@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-gru", action="store_true", help="skip the secondary CRISP-GRU measurement")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--no-conv", action="store_true", help="skip the secondary conv-model measurement")
+    ap.add_argument("--no-scl", action="store_true", help="skip the secondary SC-List measurement")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -152,6 +153,29 @@ def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
 
 
 KERNEL_NAME = "sc_fast_kernel<64>"
+
+
+def scl_measure(code, dev, y, snr, batch=1 << 18, iters=3):
+    """Secondary line: SC-List, Polar(64,32), list sizes 4 and 8, decode + fused
+    counts (npd_scl_decode_mc) on the configs[1] received words at 2 dB."""
+    yb = y[:batch].contiguous()
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    res = {}
+    for L in (4, 8):
+        code.scl_decode_mc(yb, snr, L, SEED, 0, cnt)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            code.scl_decode_mc(yb, snr, L, SEED, 0, cnt)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        res[f"L{L}"] = {"value": batch / (ms / 1e3), "avg_launch_ms": ms}
+    return {"value": res["L4"]["value"], "unit": "codewords/s", "list_size": 4, "batch": batch,
+            "avg_launch_ms": res["L4"]["avg_launch_ms"], "L8": res["L8"],
+            "bound": "VALU/LDS (per-path SC + list bookkeeping; 384 B/cw of HBM traffic is not the limit)",
+            "config": "Polar(64,32) scl_decode(L) (polar.py:793-876), 2 dB, decode + fused BER/BLER counts"}
 
 
 def conv_measure(dev, batch=8192, iters=3):
@@ -320,6 +344,8 @@ def main():
     }
     if not args.no_gru:
         out["crisp_gru"] = gru_measure(code, dev, ys[2], snrs[2])
+    if not args.no_scl:
+        out["scl"] = scl_measure(code, dev, ys[2], snrs[2])
     if not args.no_conv:
         out["conv_model"] = conv_measure(dev)
     if not args.no_traffic and world == 1:

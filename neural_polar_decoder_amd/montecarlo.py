@@ -112,6 +112,19 @@ class SCMonteCarlo(MonteCarlo):
         self.code.sc_decode_mc(y, snr, self.seed, cw_offset, counters_row)
 
 
+class SCLMonteCarlo(SCMonteCarlo):
+    """Polar SC-List decoding (polar.py:793-876, run_models.py:327-331): fused generate +
+    npd_scl_decode_mc (decode and count in one launch)."""
+
+    def __init__(self, code, list_size, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
+        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device)
+        self.list_size = int(list_size)
+
+    def count_batch(self, si, snr, cw_offset, n, counters_row):
+        _, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=False)
+        self.code.scl_decode_mc(y, snr, self.list_size, self.seed, cw_offset, counters_row)
+
+
 class GRUMonteCarlo(MonteCarlo):
     """CRISP GRU decoding (rnn_all.py:874-878): decoded[:, info] vs the message, counted on device."""
 
@@ -143,6 +156,7 @@ def _main(argv=None):
     ap.add_argument("--test_size", type=int, default=1 << 20)
     ap.add_argument("--batch_size", type=int, default=1 << 20)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--list_size", type=int, default=None, help="also run SC-List with this list size (Polar)")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
@@ -161,11 +175,21 @@ def _main(argv=None):
         code = PAC(argparse.Namespace(target_K=a.target_K or a.K), a.N, a.K, a.g)
     snrs = snr_range(a.test_snr_start, a.test_snr_end, a.snr_points)
     res = SCMonteCarlo(code, snrs, a.test_size, a.batch_size, a.seed).run()
+    scl = None
+    if a.list_size:
+        if a.code != "polar":
+            raise SystemExit("--list_size: SC-List is defined for Polar codes only (polar.py:793)")
+        scl = SCLMonteCarlo(code, a.list_size, snrs, a.test_size, a.batch_size, a.seed).run()
     if _dist() is None or _dist().get_rank() == 0:
         print("Test SNRs : ", snrs)
-        print("BERs of SC decoding: ", res.ber)
-        print("BLERs of SC decoding: ", res.bler)
-        print(json.dumps(res.as_dict()))
+        print("BERs of SC decoding: {0}".format(res.ber))
+        print("BLERs of SC decoding: {0}".format(res.bler))
+        rec = {"sc": res.as_dict()}
+        if scl is not None:
+            print("BERs of SCL decoding: {0}".format(scl.ber))
+            print("BLERs of SCL decoding: {0}".format(scl.bler))
+            rec["scl"] = dict(scl.as_dict(), list_size=a.list_size)
+        print(json.dumps(rec))
     return res
 
 

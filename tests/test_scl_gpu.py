@@ -97,3 +97,13 @@ def test_scl_list_gain_and_noiseless():
     code.scl_decode_mc(y, 2.0, 4, 3, 0, c_l4)
     bler_sc, bler_l4 = c_sc[1].item() / B, c_l4[1].item() / B
     assert bler_l4 < 0.8 * bler_sc, (bler_sc, bler_l4)
+
+
+def test_scl_montecarlo_shard_invariance():
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import SCLMonteCarlo
+    code = reference_polar_code(64, 32)
+    one = SCLMonteCarlo(code, 4, [1.0, 2.0], 30_001, 8192, seed=5, rank=0, world=1).run()
+    parts = [SCLMonteCarlo(code, 4, [1.0, 2.0], 30_001, 8192, seed=5, rank=r, world=2).run() for r in range(2)]
+    assert [sum(p.block_errors[i] for p in parts) for i in range(2)] == one.block_errors
+    assert [sum(p.bit_errors[i] for p in parts) for i in range(2)] == one.bit_errors
