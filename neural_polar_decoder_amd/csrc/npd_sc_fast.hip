@@ -19,11 +19,11 @@
 #ifndef NPD_SCF_BRANCHFREE
 #define NPD_SCF_BRANCHFREE 0
 #endif
-#ifndef NPD_SCF_DIRECT
-#define NPD_SCF_DIRECT 0  // 1: each lane loads its own row (no LDS transpose; uncoalesced 16-B pieces)
-#endif
 #ifndef NPD_SCF_ROOT_LDS
 #define NPD_SCF_ROOT_LDS 0  // 1: the root level is read from the LDS row image instead of 64 VGPRs
+#endif
+#ifndef NPD_SCF_PACKED
+#define NPD_SCF_PACKED 1  // g-updates and partial-sum products as packed fp32 pairs
 #endif
 #ifndef NPD_SCF_PREFETCH
 #define NPD_SCF_PREFETCH 1
@@ -50,9 +50,13 @@ __device__ __forceinline__ float rmul(float a, float b) {
     return r;
 }
 
+// sign(a) sign(b) min(|a|, |b|) in two VALU ops: med3(|a|, -|a|, b) = clamp(b, -|a|, |a|) has the
+// magnitude min(|a|, |b|) and the sign of b; xor in the sign of a (v_med3_f32 + v_bitop3_b32).
+// Equal in value to the reference's product form (zeros may differ only in their sign bit, which
+// no later step reads: sign(+-0) = 0, |+-0| = 0, u * (+-0) + b = b).
 __device__ __forceinline__ float f_minsum(float a, float b) {
-    const float m = __builtin_fminf(__builtin_fabsf(a), __builtin_fabsf(b));
-    return bitsf(fbits(m) | ((fbits(a) ^ fbits(b)) & 0x80000000u));
+    const float m = __builtin_amdgcn_fmed3f(__builtin_fabsf(a), -__builtin_fabsf(a), b);
+    return bitsf(fbits(m) ^ (fbits(a) & 0x80000000u));
 }
 
 __device__ __forceinline__ float sgn_bits(float x) {
@@ -61,6 +65,7 @@ __device__ __forceinline__ float sgn_bits(float x) {
 }
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int N>
 struct Lane {
@@ -76,7 +81,9 @@ struct Lane {
 template <int N, int I>
 __device__ __forceinline__ void leaf(Lane<N>& c, const CodeParams& p, float L) {
     const bool frozen = (c.fz[I >> 5] >> (I & 31)) & 1u;
-    const float lf = L + (frozen ? c.infty : 0.0f);  // polar.py:438/446
+    // prior selected on the scalar unit (frozen and infty are wave-uniform): one v_add_f32
+    const uint32_t pbits = __builtin_amdgcn_readfirstlane(frozen ? fbits(c.infty) : 0u);
+    const float lf = L + bitsf(pbits);  // polar.py:438/446
     const float u = sgn_bits(lf);                     // polar.py:479
 #if NPD_SCF_BRANCHFREE
     // branch-free: frozen decisions go to the row's padding byte (NB - 1 >= N); one basic block, but
@@ -103,12 +110,37 @@ __device__ __forceinline__ void node(Lane<N>& c, const CodeParams& p) {
 #pragma unroll
         for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
         node<N, D - 1, S0>(c, p);
+        if constexpr (h >= 2 && NPD_SCF_PACKED) {
+            // g and the partial-sum products as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth
+            // per instruction).  u * a is exact (u in {-1, 0, 1}), so the fused form equals mul + add.
 #pragma unroll
-        for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[S0 + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+            for (int j = 0; j < h; j += 2) {
+                const f2 u2 = {c.beta[S0 + j], c.beta[S0 + j + 1]};
+                const f2 a2 = {c.lv[2 * h + j], c.lv[2 * h + j + 1]};
+                const f2 b2 = {c.lv[3 * h + j], c.lv[3 * h + j + 1]};
+                const f2 r = __builtin_elementwise_fma(u2, a2, b2);
+                c.lv[h + j] = r.x;
+                c.lv[h + j + 1] = r.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[S0 + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+        }
         node<N, D - 1, S0 + h>(c, p);
         if constexpr ((1 << D) < N) {
+            if constexpr (h >= 2 && NPD_SCF_PACKED) {
 #pragma unroll
-            for (int j = 0; j < h; ++j) c.beta[S0 + j] = c.beta[S0 + j] * c.beta[S0 + h + j];
+                for (int j = 0; j < h; j += 2) {
+                    const f2 x = {c.beta[S0 + j], c.beta[S0 + j + 1]};
+                    const f2 y = {c.beta[S0 + h + j], c.beta[S0 + h + j + 1]};
+                    const f2 r = x * y;
+                    c.beta[S0 + j] = r.x;
+                    c.beta[S0 + j + 1] = r.y;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < h; ++j) c.beta[S0 + j] = c.beta[S0 + j] * c.beta[S0 + h + j];
+            }
         }
     }
 }
@@ -199,6 +231,24 @@ __device__ __forceinline__ void store_msg(const char* lds, uint32_t kU, float* m
     }
 }
 
+// chunk q of tile t for this lane = float4 index t*64*C + lane + 64*q.  Full tiles (all but possibly the
+// last) address from a wave-uniform base (SGPR) plus the lane offset: no per-chunk 64-bit clamps.
+template <int C>
+__device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4, int64_t t, int lane, int64_t B,
+                                          int64_t last4) {
+    const f4* base = y4 + t * (int64_t)(kWave * C);
+    if ((t + 1) * kWave <= B) {
+#pragma unroll
+        for (int q = 0; q < C; ++q) nx[q] = base[lane + kWave * q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < C; ++q) {
+            const int64_t gi = t * (int64_t)(kWave * C) + lane + kWave * q;
+            nx[q] = y4[gi < last4 ? gi : last4];
+        }
+    }
+}
+
 #ifdef NPD_SCF_STAMPS
 // diagnostic build only: per-phase cycle sums per wave, written to counters + 2 (never in the product)
 #define STAMP(var)                                                                     \
@@ -219,7 +269,7 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
     constexpr int C = N / 4;                 // 16-B chunks per row (and per lane per tile)
     constexpr int NB = 4 * ((N / 4) | 1);    // decision-row stride in bytes (odd dword count)
     constexpr uint32_t kStage = 0;
-    constexpr uint32_t kU = NPD_SCF_DIRECT ? 0u : (uint32_t)(kWave * N * 4);
+    constexpr uint32_t kU = (uint32_t)(kWave * N * 4);
     const int lane = threadIdx.x;
     const int K = p.K;
 
@@ -237,35 +287,15 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
     int64_t pend_row0 = 0;  // previous tile: its msg_hat stores are issued one iteration late, before the
     int pend_rows = 0;      // next prefetch, so the wait for that prefetch never waits for fresh stores
     int64_t t = blockIdx.x;
-    if (NPD_SCF_PREFETCH && t < a.ntiles) {
-#pragma unroll
-        for (int q = 0; q < C; ++q) {
-            int64_t gi = t * (int64_t)(kWave * C) + lane + kWave * q;
-            nx[q] = y4[gi < last4 ? gi : last4];
-        }
-    }
+    if (NPD_SCF_PREFETCH && t < a.ntiles) load_tile<C>(nx, y4, t, lane, a.B, last4);
     unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0;
     unsigned long long ph[4] = {0, 0, 0, 0};
     for (; t < a.ntiles; t += gridDim.x) {
         STAMP(ts0);
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
-        if (!NPD_SCF_PREFETCH) {
-#pragma unroll
-            for (int q = 0; q < C; ++q) {
-                int64_t gi = NPD_SCF_DIRECT ? (t * kWave + lane) * C + q : t * (int64_t)(kWave * C) + lane + kWave * q;
-                nx[q] = y4[gi < last4 ? gi : last4];
-            }
-        }
-        if (NPD_SCF_DIRECT) {
-#pragma unroll
-            for (int q = 0; q < C; ++q) {
-                c.lv[N + 4 * q + 0] = rmul(a.scale, nx[q].x);
-                c.lv[N + 4 * q + 1] = rmul(a.scale, nx[q].y);
-                c.lv[N + 4 * q + 2] = rmul(a.scale, nx[q].z);
-                c.lv[N + 4 * q + 3] = rmul(a.scale, nx[q].w);
-            }
-        } else {
+        if (!NPD_SCF_PREFETCH) load_tile<C>(nx, y4, t, lane, a.B, last4);
+        {
         // ---- transpose the tile through LDS: chunk (lane + 64q) -> row r = (lane + 64q)/C, col chunk
 #pragma unroll
         for (int q = 0; q < C; ++q) {
@@ -289,13 +319,7 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
         if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane);
         // ---- prefetch the next tile (lands while this one is decoded)
         const int64_t tn = t + gridDim.x;
-        if (NPD_SCF_PREFETCH && tn < a.ntiles) {
-#pragma unroll
-            for (int q = 0; q < C; ++q) {
-                int64_t gi = NPD_SCF_DIRECT ? (tn * kWave + lane) * C + q : tn * (int64_t)(kWave * C) + lane + kWave * q;
-                nx[q] = y4[gi < last4 ? gi : last4];
-            }
-        }
+        if (NPD_SCF_PREFETCH && tn < a.ntiles) load_tile<C>(nx, y4, tn, lane, a.B, last4);
         STAMP(ts2);
         // ---- decode.  The per-leaf frozen tests are loop-invariant; left alone the compiler hoists all
         // of them out of the tile loop and spills the resulting 64 SGPR pairs to VGPR lanes.  Making the
@@ -312,7 +336,7 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
             c.infty = inf;
         }
         c.slot = 0;
-        if (NPD_SCF_ROOT_LDS && !NPD_SCF_DIRECT) root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, a.scale);
+        if (NPD_SCF_ROOT_LDS) root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, a.scale);
         else node<N, n, 0>(c, p);
 
         STAMP(ts3);
@@ -370,7 +394,7 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
 template <int N>
 static int launch(const CodeParams& p, Args a, hipStream_t s) {
     constexpr int NB = 4 * ((N / 4) | 1);
-    const size_t lds = (NPD_SCF_DIRECT ? 0 : (size_t)kWave * N * 4) + (size_t)kWave * NB;
+    const size_t lds = (size_t)kWave * N * 4 + (size_t)kWave * NB;
     a.ntiles = (a.B + kWave - 1) / kWave;
     auto kern = sc_fast_kernel<N>;
     int occ = 0;
