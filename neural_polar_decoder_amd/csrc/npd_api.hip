@@ -80,6 +80,18 @@ int npd_code_create(int N, int K, const int32_t* info_sorted, int pac_g, float i
         p.rank[i] = (uint32_t)k;
         p.frozen[i >> 5] &= ~(1u << (i & 31));
     }
+    for (int D = 1; D <= p.n; ++D)
+        for (int s0 = 0; s0 < N; s0 += 1 << D) {
+            int k = 0;
+            for (int i = s0; i < s0 + (1 << D); ++i) k += ((p.frozen[i >> 5] >> (i & 31)) & 1u) ? 0 : 1;
+            const bool last_info = !((p.frozen[(s0 + (1 << D) - 1) >> 5] >> ((s0 + (1 << D) - 1) & 31)) & 1u);
+            uint32_t t = npd::kNodeMixed;
+            if (k == 0) t = npd::kNodeRate0;
+            else if (k == (1 << D)) t = npd::kNodeRate1;
+            else if (k == 1 && last_info) t = npd::kNodeRep;
+            const int id = (N >> D) + (s0 >> D);
+            p.ntype[id >> 4] |= t << (2 * (id & 15));
+        }
     if (pac_g != 0) {
         NPD_ARG(pac_g > 1, "npd_code_create: invalid PAC polynomial");
         int M = 0;

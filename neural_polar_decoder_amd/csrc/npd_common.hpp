@@ -47,7 +47,13 @@ struct CodeParams {           // passed to kernels by value (lives in SGPRs / ke
     uint32_t tapmask;             // PAC: state-index taps (bit t -> state[t] participates)
     uint32_t smask;               // PAC: (1 << state_len) - 1
     int pac;
+    // Subtree classes for the fast Polar kernel: 2 bits per node, node id = (N >> D) + (S0 >> D) for the
+    // node of 2^D leaves starting at S0 (root id 1, ids < N).  0 = mixed, 1 = rate-0 (all frozen),
+    // 2 = rate-1 (all information), 3 = repetition (only the last leaf carries information).
+    uint32_t ntype[kMaxN / 16];
 };
+
+enum NodeType : uint32_t { kNodeMixed = 0, kNodeRate0 = 1, kNodeRate1 = 2, kNodeRep = 3 };
 
 }  // namespace npd
 

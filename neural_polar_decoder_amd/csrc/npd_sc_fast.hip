@@ -12,6 +12,8 @@
 //     Philox message bits, and msg_hat leaves as coalesced 16-B stores.
 #include "npd_common.hpp"
 
+#include <cstdlib>
+
 // Tuning knobs (compile-time; defaults are the measured best on MI355X):
 #ifndef NPD_SCF_WPE
 #define NPD_SCF_WPE 2
@@ -145,6 +147,111 @@ __device__ __forceinline__ void node(Lane<N>& c, const CodeParams& p) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------- specialised codes
+// For the reference's standard Polar codes the frozen set is a compile-time constant, so the decoder is
+// unrolled against it: leaf tests, slot offsets and subtree classes are resolved at compile time, and
+// three subtree classes are decoded in closed form where that is provably identical to the step-by-step
+// SC (polar.py:465-484):
+//  * rate-0 (all frozen) and repetition (only the last leaf informative): if sum |a_j| < 999 over the
+//    subtree's input LLRs a, every leaf LLR inside has magnitude < 1000 (g adds magnitudes, f takes a
+//    minimum, all partial sums are +1), so every frozen leaf decides sign(L + 1000) = +1; the partial sums
+//    are +1 (rate-0) and the repetition node's informative leaf sees the SC-order pairwise sum of a;
+//  * rate-1 (all informative): if no a_j is 0, SC's partial sums equal sign(a) (by induction: f keeps
+//    |.| > 0, g adds two terms of equal sign) and the decisions are their Plotkin transform.
+// A lane whose inputs break a condition flags the tile; the whole tile is then decoded again by the
+// step-by-step path (reloaded from the LDS image), so results never depend on the shortcut.
+namespace spec {
+
+template <int N, uint64_t M>
+struct CT {
+    static constexpr bool frozen(int i) { return ((M >> i) & 1ull) != 0; }
+    static constexpr int rank(int i) {
+        int r = 0;
+        for (int j = 0; j < i; ++j) r += frozen(j) ? 0 : 1;
+        return r;
+    }
+    static constexpr int type(int D, int S0) {
+        int k = 0;
+        for (int i = S0; i < S0 + (1 << D); ++i) k += frozen(i) ? 0 : 1;
+        if (k == 0) return kNodeRate0;
+        if (k == (1 << D)) return kNodeRate1;
+        if (k == 1 && !frozen(S0 + (1 << D) - 1)) return kNodeRep;
+        return kNodeMixed;
+    }
+};
+
+template <int N, uint64_t M, int D, int S0>
+__device__ __forceinline__ void snode(Lane<N>& c, uint32_t& bad) {
+    using T = CT<N, M>;
+    constexpr int SZ = 1 << D;
+    if constexpr (D == 0) {
+        const float L = c.lv[1];
+        if constexpr (T::frozen(S0)) {
+            c.beta[S0] = sgn_bits(L + c.infty);  // polar.py:438/446, 479
+        } else {
+            const float u = sgn_bits(L);
+            *reinterpret_cast<int8_t*>(c.lds + c.u_row + T::rank(S0)) = (int8_t)(int)u;
+            c.beta[S0] = u;
+        }
+    } else if constexpr (T::type(D, S0) == kNodeRate0 || T::type(D, S0) == kNodeRep) {
+        float sa = 0.0f;
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) sa += __builtin_fabsf(c.lv[SZ + j]);
+        bad |= (sa < 999.0f) ? 0u : 1u;
+        if constexpr (T::type(D, S0) == kNodeRate0) {
+#pragma unroll
+            for (int j = 0; j < SZ; ++j) c.beta[S0 + j] = 1.0f;
+        } else {
+            float t[SZ];
+#pragma unroll
+            for (int j = 0; j < SZ; ++j) t[j] = c.lv[SZ + j];
+#pragma unroll
+            for (int h = SZ / 2; h >= 1; h /= 2)
+#pragma unroll
+                for (int j = 0; j < h; ++j) t[j] = t[j] + t[h + j];  // g-updates with u = +1
+            const float u = sgn_bits(t[0]);
+            *reinterpret_cast<int8_t*>(c.lds + c.u_row + T::rank(S0 + SZ - 1)) = (int8_t)(int)u;
+#pragma unroll
+            for (int j = 0; j < SZ; ++j) c.beta[S0 + j] = u;
+        }
+    } else if constexpr (T::type(D, S0) == kNodeRate1) {
+        float m = __builtin_fabsf(c.lv[SZ]);
+#pragma unroll
+        for (int j = 1; j < SZ; ++j) m = __builtin_fminf(m, __builtin_fabsf(c.lv[SZ + j]));
+        bad |= (m > 0.0f) ? 0u : 1u;
+        float b[SZ];
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) {
+            b[j] = bitsf((fbits(c.lv[SZ + j]) & 0x80000000u) | 0x3f800000u);
+            c.beta[S0 + j] = b[j];
+        }
+#pragma unroll
+        for (int st = 1; st < SZ; st *= 2)
+#pragma unroll
+            for (int i = 0; i < SZ; i += 2 * st)
+#pragma unroll
+                for (int j = 0; j < st; ++j) b[i + j] = b[i + j] * b[i + st + j];
+#pragma unroll
+        for (int j = 0; j < SZ; ++j)
+            *reinterpret_cast<int8_t*>(c.lds + c.u_row + T::rank(S0) + j) = (int8_t)(int)b[j];
+    } else {
+        constexpr int h = SZ / 2;
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
+        snode<N, M, D - 1, S0>(c, bad);
+#pragma unroll
+        for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[S0 + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+        snode<N, M, D - 1, S0 + h>(c, bad);
+        if constexpr (SZ < N) {
+#pragma unroll
+            for (int j = 0; j < h; ++j) c.beta[S0 + j] = c.beta[S0 + j] * c.beta[S0 + h + j];
+        }
+    }
+}
+
+}  // namespace spec
+
 template <int N>
 constexpr int log2c() {
     int n = 0;
@@ -262,7 +369,7 @@ __device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4
 #else
 #define STAMP(var) do { } while (0)
 #endif
-template <int N>
+template <int N, uint64_t MASK = 0, bool SPEC = false>
 __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
@@ -336,8 +443,28 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
             c.infty = inf;
         }
         c.slot = 0;
-        if (NPD_SCF_ROOT_LDS) root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, a.scale);
-        else node<N, n, 0>(c, p);
+        if constexpr (SPEC) {
+            uint32_t bad = 0;
+            spec::snode<N, MASK, n, 0>(c, bad);
+            if (__ballot(bad != 0u) != 0ull) {
+                // a shortcut's precondition failed on some lane (huge or zero LLRs): decode the tile again
+                // step by step from the LDS image of its received words
+#pragma unroll
+                for (int q = 0; q < C; ++q) {
+                    const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
+                    c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
+                    c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
+                    c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
+                    c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+                }
+                c.slot = 0;
+                node<N, n, 0>(c, p);
+            }
+        } else if (NPD_SCF_ROOT_LDS) {
+            root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, a.scale);
+        } else {
+            node<N, n, 0>(c, p);
+        }
 
         STAMP(ts3);
         // ---- error count: 4 slots per dword vs the Philox message bits (errors_ber/bler semantics)
@@ -391,12 +518,12 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
     }
 }
 
-template <int N>
+template <int N, uint64_t MASK = 0, bool SPEC = false>
 static int launch(const CodeParams& p, Args a, hipStream_t s) {
     constexpr int NB = 4 * ((N / 4) | 1);
     const size_t lds = (size_t)kWave * N * 4 + (size_t)kWave * NB;
     a.ntiles = (a.B + kWave - 1) / kWave;
-    auto kern = sc_fast_kernel<N>;
+    auto kern = sc_fast_kernel<N, MASK, SPEC>;
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, lds) != hipSuccess || occ <= 0) {
         (void)hipGetLastError();
@@ -408,6 +535,17 @@ static int launch(const CodeParams& p, Args a, hipStream_t s) {
 }
 
 }  // namespace scf
+
+// (N, frozen mask) of the specialised codes: PolarCode 'polar' profile (run_models.py:630-639), K = N/2
+#define NPD_SPEC_CODES(X) X(64, 0x1013f037f7fff) X(32, 0x117177f) X(16, 0x17f) X(8, 0x17)
+
+static bool spec_disabled() {
+    static const bool off = [] {
+        const char* e = getenv("NPD_SC_NOSPEC");
+        return e && e[0] == '1';
+    }();
+    return off;
+}
 
 // eligible: Polar, 8 <= N <= 64, K <= 128 (one Philox block of message bits), y 16-B aligned
 bool sc_fast_eligible(const CodeParams& p, const void* y) {
@@ -425,6 +563,16 @@ int sc_fast_run(const CodeParams& p, const float* y, float llr_scale, float* msg
     a.B = B;
     a.scale = llr_scale;
     a.count = counters ? 1u : 0u;
+    // the reference's standard codes ('polar' rate profile, K = N/2) have specialised decoders
+    if (!spec_disabled() && p.N <= 64) {
+        uint64_t m = 0;
+        for (int i = 0; i < p.N; ++i)
+            if ((p.frozen[i >> 5] >> (i & 31)) & 1u) m |= 1ull << i;
+#define NPD_SPEC(NN, MM) \
+        if (p.N == NN && m == MM##ull) return scf::launch<NN, MM##ull, true>(p, a, s);
+        NPD_SPEC_CODES(NPD_SPEC)
+#undef NPD_SPEC
+    }
     switch (p.N) {
         case 8: return scf::launch<8>(p, a, s);
         case 16: return scf::launch<16>(p, a, s);

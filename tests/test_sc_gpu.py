@@ -258,3 +258,30 @@ def test_montecarlo_pac_and_gru_drivers_run():
     dec = RNN_decoder("y_input", 64, code.info_positions, onehot=True)
     g = GRUMonteCarlo(code, net, dec, [0.0, 4.0], 2048, 1024).run()
     assert all(0.3 < b < 0.7 for b in g.ber)  # untrained weights: coin flips
+
+
+@pytest.mark.parametrize("N,K", [(64, 32), (32, 16), (16, 8)])
+def test_msg_only_fast_paths_on_golden_including_crafted_rows(N, K):
+    """msg-only decoding takes the streaming kernels (for these standard codes the frozen-set-specialised
+    one, whose closed-form subtrees fall back to step-by-step SC on huge or zero LLRs): same msg_hat as
+    the reference on every golden row, including the crafted zero / |LLR| >> 1000 rows."""
+    d = golden(f"sc_polar_{N}_{K}.npz")
+    code = polar_for(N, d["info"])
+    for s in np.unique(d["snr"]):
+        m = d["snr"] == s
+        y = t(d["y"][m])
+        assert np.array_equal(code.sc_decode_msg(y, float(s)).cpu().numpy(), d["msg_hat"][m]), (N, s)
+        cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+        hat = torch.empty(y.shape[0], K, device=DEV)
+        code.sc_decode_mc(y, float(s), 1, 0, cnt, msg_hat=hat)
+        assert np.array_equal(hat.cpu().numpy(), d["msg_hat"][m]), (N, s)
+
+
+def test_specialised_8_4_and_high_snr_vs_oracle(oracle):
+    from neural_polar_decoder_amd import reference_polar_code
+    for N, K in [(8, 4), (64, 32), (32, 16)]:
+        code = reference_polar_code(N, K)
+        for snr in (-2.0, 6.0, 12.0):
+            _, _, y = code.mc_generate(20000, snr, seed=4, want_msg=False)
+            _, oh = oracle.sc_decode(y.cpu().numpy(), snr, code.info_positions)
+            assert np.array_equal(code.sc_decode_msg(y, snr).cpu().numpy(), oh), (N, snr)
