@@ -18,6 +18,9 @@
 #ifndef NPD_SCF_WPE
 #define NPD_SCF_WPE 2
 #endif
+#ifndef NPD_SCF_WPB
+#define NPD_SCF_WPB 8  // waves per workgroup (each with its own LDS tile; they share only the counter reduction)
+#endif
 #ifndef NPD_SCF_BRANCHFREE
 #define NPD_SCF_BRANCHFREE 0
 #endif
@@ -26,6 +29,10 @@
 #endif
 #ifndef NPD_SCF_PACKED
 #define NPD_SCF_PACKED 1  // g-updates and partial-sum products as packed fp32 pairs
+#endif
+#ifndef NPD_SCF_ABL
+#define NPD_SCF_ABL 0  // diagnostic builds only: 1 = skip the decode, 2 = skip the loads after the first tile,
+                       // 3 = loads + transposition only, 4 = loads only
 #endif
 #ifndef NPD_SCF_PREFETCH
 #define NPD_SCF_PREFETCH 1
@@ -58,7 +65,7 @@ __device__ __forceinline__ float rmul(float a, float b) {
 // no later step reads: sign(+-0) = 0, |+-0| = 0, u * (+-0) + b = b).
 __device__ __forceinline__ float f_minsum(float a, float b) {
     const float m = __builtin_amdgcn_fmed3f(__builtin_fabsf(a), -__builtin_fabsf(a), b);
-    return bitsf(fbits(m) ^ (fbits(a) & 0x80000000u));
+    return bitsf(__builtin_amdgcn_bitop3_b32(fbits(m), fbits(a), 0x80000000u, 0x78));  // m ^ (a & 0x80000000)
 }
 
 __device__ __forceinline__ float sgn_bits(float x) {
@@ -300,27 +307,37 @@ __device__ __forceinline__ void root_lds(Lane<N>& c, const CodeParams& p, const 
 // msg_hat of one finished tile: its rows*K floats are contiguous in HBM; decisions are int8 in slot order
 template <int N>
 __device__ __forceinline__ void store_msg(const char* lds, uint32_t kU, float* msg, int64_t row0, int rows, int K,
-                                          int lane) {
-    constexpr int NB = 4 * ((N / 4) | 1);
+                                          int lane, int NB) {
     float* dst = msg + row0 * (int64_t)K;
     const int total = rows * K;
     if ((K & 3) == 0) {
-        int f = 4 * lane;
-        int r = f / K, col = f % K;
+        // batches of 4: the LDS reads first, then the conversions and 16-B stores (one wait per batch)
+        int r = (4 * lane) / K, col = (4 * lane) % K;
         const int dr = 256 / K, dc = 256 % K;
-        for (; f < total; f += 256) {
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(lds + kU + (uint32_t)(r * NB + col));
-            f4 o;
-            o.x = (float)(int8_t)(w & 0xFFu);
-            o.y = (float)(int8_t)((w >> 8) & 0xFFu);
-            o.z = (float)(int8_t)((w >> 16) & 0xFFu);
-            o.w = (float)(int8_t)(w >> 24);
-            *reinterpret_cast<f4*>(dst + f) = o;
-            r += dr;
-            col += dc;
-            if (col >= K) {
-                col -= K;
-                ++r;
+        for (int f0 = 4 * lane; f0 < total; f0 += 4 * 256) {
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[i] = (f0 + 256 * i < total) ? *reinterpret_cast<const uint32_t*>(lds + kU + (uint32_t)(r * NB + col))
+                                              : 0u;
+                r += dr;
+                col += dc;
+                if (col >= K) {
+                    col -= K;
+                    ++r;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int f = f0 + 256 * i;
+                if (f < total) {
+                    f4 o;
+                    o.x = (float)(int8_t)(w[i] & 0xFFu);
+                    o.y = (float)(int8_t)((w[i] >> 8) & 0xFFu);
+                    o.z = (float)(int8_t)((w[i] >> 16) & 0xFFu);
+                    o.w = (float)(int8_t)(w[i] >> 24);
+                    *reinterpret_cast<f4*>(dst + f) = o;
+                }
             }
         }
     } else {
@@ -369,16 +386,26 @@ __device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4
 #else
 #define STAMP(var) do { } while (0)
 #endif
+// decision-row stride: an odd number of dwords holding the K slot bytes (conflict-free dword reads)
+__host__ __device__ constexpr int row_stride(int K) { return 4 * ((((K > 0 ? K : 1) + 3) / 4) | 1); }
+
 template <int N, uint64_t MASK = 0, bool SPEC = false>
-__global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodeParams p, const Args a) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+__global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) void sc_fast_kernel(const CodeParams p,
+                                                                                                   const Args a) {
+    constexpr int KC = N - __builtin_popcountll(MASK);  // information bits of a specialised code
+    extern __shared__ __attribute__((aligned(16))) char lds_all[];
     constexpr int n = log2c<N>();
     constexpr int C = N / 4;                 // 16-B chunks per row (and per lane per tile)
-    constexpr int NB = 4 * ((N / 4) | 1);    // decision-row stride in bytes (odd dword count)
+    const int K = p.K;
+    const int NB = SPEC ? row_stride(KC) : row_stride(K);
+    const int wpb = blockDim.x >> 6;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    // per-wave LDS: the staged tile (64 rows x N fp32) then 64 decision rows of NB bytes
+    const uint32_t per_wave = (uint32_t)(kWave * N * 4 + kWave * NB);
+    char* lds = lds_all + wave * per_wave;
     constexpr uint32_t kStage = 0;
     constexpr uint32_t kU = (uint32_t)(kWave * N * 4);
-    const int lane = threadIdx.x;
-    const int K = p.K;
 
     Lane<N> c;
     c.lds = lds;
@@ -393,14 +420,30 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
     f4 nx[C];
     int64_t pend_row0 = 0;  // previous tile: its msg_hat stores are issued one iteration late, before the
     int pend_rows = 0;      // next prefetch, so the wait for that prefetch never waits for fresh stores
-    int64_t t = blockIdx.x;
+    int64_t t = (int64_t)blockIdx.x * wpb + wave;
+    int64_t gstride = (int64_t)gridDim.x * wpb;
+    asm volatile("" : "+s"(gstride));  // keep the grid stride in SGPRs (otherwise re-read every tile)
     if (NPD_SCF_PREFETCH && t < a.ntiles) load_tile<C>(nx, y4, t, lane, a.B, last4);
-    unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0;
-    unsigned long long ph[4] = {0, 0, 0, 0};
-    for (; t < a.ntiles; t += gridDim.x) {
+    unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0;
+    unsigned long long ph[5] = {0, 0, 0, 0, 0};
+    for (; t < a.ntiles; t += gstride) {
         STAMP(ts0);
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
+        // ---- this tile's message bits (Philox, pure VALU) first: it fills the wait for the tile's data.
+        // The seed is made opaque per tile so the key schedule is recomputed with scalar adds here
+        // instead of being hoisted into 20 loop-invariant SGPRs (which spill to VGPR lanes).
+        uint32_t mw[4] = {0u, 0u, 0u, 0u};
+        if (a.count && NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4) {
+            uint64_t sd = a.seed;
+            asm volatile("" : "+s"(sd));
+            const u32x4 o = philox_block(sd, kStreamMsg, a.cw_offset + (uint64_t)(row0 + lane), 0u);
+            mw[0] = o.x;
+            mw[1] = o.y;
+            mw[2] = o.z;
+            mw[3] = o.w;
+        }
+        STAMP(ts1);
         if (!NPD_SCF_PREFETCH) load_tile<C>(nx, y4, t, lane, a.B, last4);
         {
         // ---- transpose the tile through LDS: chunk (lane + 64q) -> row r = (lane + 64q)/C, col chunk
@@ -408,9 +451,20 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
         for (int q = 0; q < C; ++q) {
             const int pch = lane + kWave * q;
             const int r = pch / C, cc = pch % C;
-            *reinterpret_cast<f4*>(lds + kStage + 16u * (uint32_t)(r * C + (cc ^ swz<C>(r)))) = nx[q];
+            if (NPD_SCF_ABL == 4) {
+                if (nx[q].x == 123.f) *reinterpret_cast<f4*>(lds + kStage) = nx[q];
+            } else {
+                *reinterpret_cast<f4*>(lds + kStage + 16u * (uint32_t)(r * C + (cc ^ swz<C>(r)))) = nx[q];
+            }
         }
-        if (!NPD_SCF_ROOT_LDS) {
+        // ---- prefetch the next tile as soon as its registers are free (lands while this one is decoded)
+        if (NPD_SCF_PREFETCH && NPD_SCF_ABL != 2 && t + gstride < a.ntiles)
+            load_tile<C>(nx, y4, t + gstride, lane, a.B, last4);
+        STAMP(ts2);
+        // ---- previous tile's msg_hat (its decision rows are read before this tile's leaves overwrite them;
+        // done before this tile's LLRs occupy registers)
+        if (NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4 && a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane, NB);
+        if (!NPD_SCF_ROOT_LDS && NPD_SCF_ABL < 4) {
 #pragma unroll
             for (int q = 0; q < C; ++q) {
                 const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
@@ -421,29 +475,27 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
             }
         }
         }
-        STAMP(ts1);
-        // ---- previous tile's msg_hat (its decision rows are read before this tile's leaves overwrite them)
-        if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane);
-        // ---- prefetch the next tile (lands while this one is decoded)
-        const int64_t tn = t + gridDim.x;
-        if (NPD_SCF_PREFETCH && tn < a.ntiles) load_tile<C>(nx, y4, tn, lane, a.B, last4);
-        STAMP(ts2);
+        STAMP(ts3);
         // ---- decode.  The per-leaf frozen tests are loop-invariant; left alone the compiler hoists all
         // of them out of the tile loop and spills the resulting 64 SGPR pairs to VGPR lanes.  Making the
         // frozen words opaque per tile keeps each test a single s_bitcmp next to its leaf.
+        auto frozen_words = [&] {
 #pragma unroll
-        for (int w = 0; w < (N + 31) / 32; ++w) {
-            uint32_t fw = p.frozen[w];
-            asm volatile("" : "+s"(fw));
-            c.fz[w] = fw;
-        }
+            for (int w = 0; w < (N + 31) / 32; ++w) {
+                uint32_t fw = p.frozen[w];
+                asm volatile("" : "+s"(fw));
+                c.fz[w] = fw;
+            }
+        };
+        if constexpr (!SPEC) frozen_words();
         {
             float inf = p.infty;
             asm volatile("" : "+s"(inf));
             c.infty = inf;
         }
         c.slot = 0;
-        if constexpr (SPEC) {
+        if constexpr (NPD_SCF_ABL == 1 || NPD_SCF_ABL == 3 || NPD_SCF_ABL == 4) {
+        } else if constexpr (SPEC) {
             uint32_t bad = 0;
             spec::snode<N, MASK, n, 0>(c, bad);
             if (__ballot(bad != 0u) != 0ull) {
@@ -458,6 +510,7 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
                     c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
                 }
                 c.slot = 0;
+                frozen_words();
                 node<N, n, 0>(c, p);
             }
         } else if (NPD_SCF_ROOT_LDS) {
@@ -466,24 +519,25 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
             node<N, n, 0>(c, p);
         }
 
-        STAMP(ts3);
+        STAMP(ts4);
         // ---- error count: 4 slots per dword vs the Philox message bits (errors_ber/bler semantics)
-        if (a.count) {
-            const uint64_t cw = a.cw_offset + (uint64_t)(row0 + lane);
-            const u32x4 o = philox_block(a.seed, kStreamMsg, cw, 0u);
-            const uint32_t mw[4] = {o.x, o.y, o.z, o.w};
+        if (a.count && NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4) {
+            // all decision dwords first (reads past slot K land in the next row or the slack after the last
+            // wave's rows and are masked out), then branch-free masking: slots >= K contribute nothing
+            uint32_t dec[N / 4];
+#pragma unroll
+            for (int w = 0; w < N / 4; ++w)
+                dec[w] = NPD_SCF_ABL == 6 ? mw[1] : *reinterpret_cast<const uint32_t*>(lds + c.u_row + 4 * w);
             uint32_t e = 0;
 #pragma unroll
             for (int w = 0; w < N / 4; ++w) {
-                if (4 * w < K) {
-                    const uint32_t dec = *reinterpret_cast<const uint32_t*>(lds + c.u_row + 4 * w);
-                    const uint32_t nib = (mw[(4 * w) >> 5] >> ((4 * w) & 31)) & 0xFu;
-                    const uint32_t x = (nib * 0x00204081u) & 0x01010101u;  // bit i -> byte i
-                    const uint32_t expect = 0x01010101u | (x * 0xFEu);       // +1 -> 0x01, -1 -> 0xFF
-                    const int valid = K - 4 * w;                               // slots in this dword
-                    const uint32_t vmask = valid >= 4 ? 0xFFFFFFFFu : ((1u << (8 * valid)) - 1u);
-                    e += nz_bytes((dec ^ expect) & vmask);
-                }
+                if (SPEC && 4 * w >= KC) continue;
+                const uint32_t nib = (mw[(4 * w) >> 5] >> ((4 * w) & 31)) & 0xFu;
+                const uint32_t x = (nib * 0x00204081u) & 0x01010101u;  // bit i -> byte i
+                const uint32_t expect = 0x01010101u | ((x << 8) - x);  // +1 -> 0x01, -1 -> 0xFF
+                const int valid = (SPEC ? KC : K) - 4 * w;                 // slots in this dword
+                const uint32_t vmask = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+                e += nz_bytes((dec[w] ^ expect) & vmask);
             }
             if (lane < rows) {
                 err_bits += e;
@@ -491,46 +545,71 @@ __global__ __launch_bounds__(64, NPD_SCF_WPE) void sc_fast_kernel(const CodePara
             }
         }
 
-        STAMP(ts4);
-        ph[0] += ts1 - ts0;  // wait for the tile + transpose
-        ph[1] += ts2 - ts1;  // previous tile's stores + prefetch issue
-        ph[2] += ts3 - ts2;  // SC decode
-        ph[3] += ts4 - ts3;  // error count
+        STAMP(ts5);
+        ph[0] += ts1 - ts0;  // message bits (Philox)
+        ph[1] += ts2 - ts1;  // wait for the tile, transposition writes, next prefetch issue
+        ph[2] += ts3 - ts2;  // previous tile's msg_hat stores, row reads
+        ph[3] += ts4 - ts3;  // SC decode
+        ph[4] += ts5 - ts4;  // error count
         pend_row0 = row0;
         pend_rows = rows;
     }
 #ifdef NPD_SCF_STAMPS
     if (lane == 0 && a.counters) {
-        for (int i = 0; i < 4; ++i) atomicAdd(a.counters + 2 + i, ph[i]);
-        atomicAdd(a.counters + 6, 1ull);
+        for (int i = 0; i < 5; ++i) atomicAdd(a.counters + 2 + i, ph[i]);
+        atomicAdd(a.counters + 7, 1ull);
     }
 #endif
     // the last tile's msg_hat
-    if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane);
+    if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane, NB);
 
-    if (a.count) {
+    if (a.count && NPD_SCF_ABL != 5) {
+        // one pair of device atomics per workgroup: same-address atomics from every wave serialise at
+        // the memory side and cost ~20 us per launch
         const uint32_t eb = wave_sum_u32(err_bits);
         const uint32_t bl = wave_sum_u32(err_blocks);
+        uint32_t* red = reinterpret_cast<uint32_t*>(lds_all + wpb * per_wave + N);
         if (lane == 0) {
-            atomicAdd(a.counters + 0, (unsigned long long)eb);
-            atomicAdd(a.counters + 1, (unsigned long long)bl);
+            red[2 * wave] = eb;
+            red[2 * wave + 1] = bl;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long se = 0, sb = 0;
+            for (int w = 0; w < wpb; ++w) {
+                se += red[2 * w];
+                sb += red[2 * w + 1];
+            }
+            atomicAdd(a.counters + 0, se);
+            atomicAdd(a.counters + 1, sb);
         }
     }
 }
 
 template <int N, uint64_t MASK = 0, bool SPEC = false>
 static int launch(const CodeParams& p, Args a, hipStream_t s) {
-    constexpr int NB = 4 * ((N / 4) | 1);
-    const size_t lds = (size_t)kWave * N * 4 + (size_t)kWave * NB;
+    constexpr int KC = N - __builtin_popcountll(MASK);
+    const int NB = row_stride(SPEC ? KC : p.K);
+    const size_t per_wave = (size_t)kWave * N * 4 + (size_t)kWave * NB;
+    // as many waves per workgroup as fit (up to NPD_SCF_WPB): fewer workgroups -> fewer counter atomics
+    int wpb = NPD_SCF_WPB;
+    while (wpb > 1 && (size_t)wpb * per_wave + N + 8 * wpb > 160 * 1024) --wpb;
+    const size_t lds = (size_t)wpb * per_wave + N + 8 * wpb;
     a.ntiles = (a.B + kWave - 1) / kWave;
     auto kern = sc_fast_kernel<N, MASK, SPEC>;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, lds) != hipSuccess || occ <= 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave * wpb, lds) != hipSuccess || occ <= 0) {
         (void)hipGetLastError();
         occ = 1;
     }
-    const int grid = grid_for(a.ntiles, occ, device_cu_count());
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, s, p, a);
+    const int64_t groups = (a.ntiles + wpb - 1) / wpb;
+    const int grid = grid_for(groups, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave * wpb), lds, s, p, a);
     return launch_check("sc_fast_kernel launch");
 }
 
