@@ -211,11 +211,14 @@ def traffic_child(args):
     from neural_polar_decoder_amd import reference_polar_code
     code = reference_polar_code(N_CODE, K_CODE)
     B = args.batch
-    _, _, y = code.mc_generate(B, 2.0, SEED, 2, 0, device=dev, want_msg=False)
-    hat = torch.empty(B, K_CODE, dtype=torch.float32, device=dev)
-    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    snrs = [float(s) for s in args.snrs.split(",")]
+    yall = torch.empty(len(snrs), B, N_CODE, dtype=torch.float32, device=dev)
+    for si, snr in enumerate(snrs):
+        code.mc_generate(B, snr, SEED, si, 0, want_msg=False, out=yall[si])
+    hat = torch.empty(len(snrs), B, K_CODE, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     for _ in range(4):
-        code.sc_decode_mc(y, 2.0, SEED, 0, cnt, msg_hat=hat)
+        code.sc_decode_mc_sweep(yall, snrs, SEED, 0, cnt, msg_hat=hat)
     torch.cuda.synchronize()
 
 
@@ -237,7 +240,7 @@ def pmc_traffic(args, timeout_s=240):
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(tmp, ctr)
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p", "--", sys.executable,
-               os.path.abspath(__file__), "--traffic-child", "--batch", str(args.batch)]
+               os.path.abspath(__file__), "--traffic-child", "--batch", str(args.batch), "--snrs", args.snrs]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env, cwd=ROOT)
         except Exception as e:  # noqa: BLE001
@@ -266,28 +269,28 @@ def main():
     snrs = [float(s) for s in args.snrs.split(",")]
     B = args.batch
     cw0 = rank * B  # weak scaling: every rank owns its own codeword range
-    ys = []
+    # the received words of every SNR point, back to back (n_snr, B, N), resident before timing
+    yall = torch.empty(len(snrs), B, N_CODE, dtype=torch.float32, device=dev)
     for si, snr in enumerate(snrs):
-        _, _, y = code.mc_generate(B, snr, SEED, si, cw0, device=dev, want_msg=False)
-        ys.append(y)
-    hat = torch.empty(B, K_CODE, dtype=torch.float32, device=dev)
+        code.mc_generate(B, snr, SEED, si, cw0, want_msg=False, out=yall[si])
+    ys = [yall[si] for si in range(len(snrs))]
+    hat = torch.empty(len(snrs), B, K_CODE, dtype=torch.float32, device=dev)
     counters = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def step(events=None):
-        for si, snr in enumerate(snrs):
-            if events is not None:
-                events[si][0].record(stream)
-            code.sc_decode_mc(ys[si], snr, SEED, cw0, counters[si], msg_hat=hat)
-            if events is not None:
-                events[si][1].record(stream)
+        # one step = the whole SNR sweep of the batch, one launch (npd_sc_decode_mc_sweep)
+        if events is not None:
+            events[0][0].record(stream)
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, counters, msg_hat=hat)
+        if events is not None:
+            events[0][1].record(stream)
 
     for _ in range(args.warmup):
         step()
     counters.zero_()
     torch.cuda.synchronize()
-    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in snrs]
-          for _ in range(args.steps)]
+    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]] for _ in range(args.steps)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -304,7 +307,7 @@ def main():
 
     total_cw = world * args.steps * len(snrs) * B
     value = total_cw / elapsed
-    achieved = BYTES_PER_CW * B / avg_launch_s / 1e9
+    achieved = BYTES_PER_CW * B * len(snrs) / avg_launch_s / 1e9
 
     # BER/BLER per SNR vs the reference anchors (steps x world x B codewords per SNR)
     cnt = counters.cpu().numpy()
@@ -336,8 +339,8 @@ def main():
                    "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": KERNEL_NAME + " (npd_sc_decode_mc)",
-                     "algorithmic_bytes_per_launch": BYTES_PER_CW * B, "avg_launch_ms": avg_launch_s * 1e3},
+                     "kernel": KERNEL_NAME + " (npd_sc_decode_mc_sweep: all SNR points in one launch)",
+                     "algorithmic_bytes_per_launch": BYTES_PER_CW * B * len(snrs), "avg_launch_ms": avg_launch_s * 1e3},
         "ber": {str(s): ber[s] for s in snrs},
         "bler": {str(s): bler[s] for s in snrs},
         "ber_match": bool(ber_match),

@@ -132,6 +132,15 @@ int npd_scl_decode_mc(const npd_code* code, const float* y, float llr_scale, int
  */
 int npd_list_prune_select(const float* neg_metrics, int n, int keep, uint32_t* mask_out);
 
+/*
+ * A whole SNR sweep of npd_sc_decode_mc in one launch: y is (n_snr, B, N) -- the received words of
+ * the same codewords cw_offset .. cw_offset+B-1 at n_snr SNR points (the reference's per-SNR loop,
+ * run_models.py:318-371), llr_scale a HOST array of n_snr scales, msg_hat (n_snr, B, K) or NULL,
+ * counters (n_snr, 2).  1 <= n_snr <= 16.  Same results as n_snr separate npd_sc_decode_mc calls.
+ */
+int npd_sc_decode_mc_sweep(const npd_code* code, int n_snr, const float* y, const float* llr_scale, float* msg_hat,
+                           uint64_t seed, uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream);
+
 /* ---------------------------------------------------------------------------------- counters */
 /*
  * counters[0] += #(round(ref) != round(hat)), counters[1] += #rows with any such element, over

@@ -587,8 +587,8 @@ using namespace npd;
 
 namespace npd {
 bool sc_fast_eligible(const CodeParams& p, const void* y);
-int sc_fast_run(const CodeParams& p, const float* y, float llr_scale, float* msg, unsigned long long* counters,
-                uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s);
+int sc_fast_run(const CodeParams& p, const float* y, const float* llr_scale, int n_seg, float* msg,
+                unsigned long long* counters, uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s);
 }  // namespace npd
 
 static bool fast_disabled() {
@@ -616,7 +616,7 @@ extern "C" int npd_sc_decode(const npd_code* code, const float* y, float llr_sca
     a.scale = llr_scale;
     a.flags = (leaf_llr ? sc::kLeaf : 0u) | (msg_hat ? sc::kMsg : 0u) | (u_hat ? sc::kUhat : 0u) | (gt ? sc::kGt : 0u);
     if (!leaf_llr && !u_hat && !gt && B > 0 && !fast_disabled() && sc_fast_eligible(code->p, y))
-        return sc_fast_run(code->p, y, llr_scale, msg_hat, nullptr, 0, 0, B, (hipStream_t)stream);
+        return sc_fast_run(code->p, y, &llr_scale, 1, msg_hat, nullptr, 0, 0, B, (hipStream_t)stream);
     return sc::run(code, a, (hipStream_t)stream);
 }
 
@@ -636,6 +636,28 @@ extern "C" int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_
     a.scale = llr_scale;
     a.flags = sc::kCount | (msg_hat ? sc::kMsg : 0u);
     if (B > 0 && !fast_disabled() && sc_fast_eligible(code->p, y))
-        return sc_fast_run(code->p, y, llr_scale, msg_hat, counters, seed, cw_offset, B, (hipStream_t)stream);
+        return sc_fast_run(code->p, y, &llr_scale, 1, msg_hat, counters, seed, cw_offset, B, (hipStream_t)stream);
     return sc::run(code, a, (hipStream_t)stream);
+}
+
+extern "C" int npd_sc_decode_mc_sweep(const npd_code* code, int n_snr, const float* y, const float* llr_scale,
+                                      float* msg_hat, uint64_t seed, uint64_t cw_offset, int64_t B,
+                                      unsigned long long* counters, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_decode_mc_sweep: code is NULL");
+    NPD_ARG(n_snr >= 1 && n_snr <= 16, "npd_sc_decode_mc_sweep: 1 <= n_snr <= 16");
+    NPD_ARG(llr_scale != nullptr, "npd_sc_decode_mc_sweep: llr_scale is NULL");
+    NPD_ARG(B >= 0, "npd_sc_decode_mc_sweep: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_mc_sweep: y is NULL");
+    NPD_ARG(counters != nullptr, "npd_sc_decode_mc_sweep: counters is NULL");
+    if (B == 0) return NPD_OK;
+    if (!fast_disabled() && sc_fast_eligible(code->p, y))
+        return sc_fast_run(code->p, y, llr_scale, n_snr, msg_hat, counters, seed, cw_offset, B, (hipStream_t)stream);
+    const int N = code->p.N, K = code->p.K;
+    for (int i = 0; i < n_snr; ++i) {
+        const int rc = npd_sc_decode_mc(code, y + (int64_t)i * B * N, llr_scale[i],
+                                        msg_hat ? msg_hat + (int64_t)i * B * K : nullptr, seed, cw_offset, B,
+                                        counters + 2 * i, stream);
+        if (rc) return rc;
+    }
+    return NPD_OK;
 }

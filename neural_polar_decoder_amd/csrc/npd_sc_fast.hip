@@ -21,6 +21,12 @@
 #ifndef NPD_SCF_WPB
 #define NPD_SCF_WPB 8  // waves per workgroup (each with its own LDS tile; they share only the counter reduction)
 #endif
+#ifndef NPD_SCF_NTS
+#define NPD_SCF_NTS 0  // non-temporal msg_hat stores
+#endif
+#ifndef NPD_SCF_NTL
+#define NPD_SCF_NTL 0  // non-temporal y loads
+#endif
 #ifndef NPD_SCF_BRANCHFREE
 #define NPD_SCF_BRANCHFREE 0
 #endif
@@ -41,15 +47,20 @@
 namespace npd {
 namespace scf {
 
+constexpr int kMaxSeg = 16;  // SNR points of one sweep launch
+
+// A launch decodes n_seg segments of B codewords each (the SNR points of a Monte-Carlo sweep), stored
+// back to back: y (n_seg, B, N), msg (n_seg, B, K), counters (n_seg, 2).  n_seg = 1 is the plain call.
 struct Args {
     const float* y;
-    float* msg;                      // (B,K) or null
-    unsigned long long* counters;    // {bit errors, block errors} or null
+    float* msg;                      // (n_seg, B, K) or null
+    unsigned long long* counters;    // (n_seg, 2) {bit errors, block errors} or null
     uint64_t seed;
     uint64_t cw_offset;
     int64_t B;
-    int64_t ntiles;
-    float scale;
+    int64_t ntiles;                  // tiles per segment
+    float scale[kMaxSeg];
+    int n_seg;
     uint32_t count;
 };
 
@@ -336,7 +347,11 @@ __device__ __forceinline__ void store_msg(const char* lds, uint32_t kU, float* m
                     o.y = (float)(int8_t)((w[i] >> 8) & 0xFFu);
                     o.z = (float)(int8_t)((w[i] >> 16) & 0xFFu);
                     o.w = (float)(int8_t)(w[i] >> 24);
+#if NPD_SCF_NTS
+                    __builtin_nontemporal_store(o, reinterpret_cast<f4*>(dst + f));
+#else
                     *reinterpret_cast<f4*>(dst + f) = o;
+#endif
                 }
             }
         }
@@ -363,7 +378,13 @@ __device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4
     const f4* base = y4 + t * (int64_t)(kWave * C);
     if ((t + 1) * kWave <= B) {
 #pragma unroll
-        for (int q = 0; q < C; ++q) nx[q] = base[lane + kWave * q];
+        for (int q = 0; q < C; ++q) {
+#if NPD_SCF_NTL
+            nx[q] = __builtin_nontemporal_load(base + lane + kWave * q);
+#else
+            nx[q] = base[lane + kWave * q];
+#endif
+        }
     } else {
 #pragma unroll
         for (int q = 0; q < C; ++q) {
@@ -399,7 +420,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
     const int K = p.K;
     const int NB = SPEC ? row_stride(KC) : row_stride(K);
     const int wpb = blockDim.x >> 6;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
     const int lane = threadIdx.x & 63;
     // per-wave LDS: the staged tile (64 rows x N fp32) then 64 decision rows of NB bytes
     const uint32_t per_wave = (uint32_t)(kWave * N * 4 + kWave * NB);
@@ -413,21 +434,54 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
     const int sw = swz<C>(lane);
 
     uint32_t err_bits = 0, err_blocks = 0;
-    const f4* y4 = reinterpret_cast<const f4*>(a.y);
-    const int64_t last4 = a.B * C - 1;  // last valid float4 of y
+    // per-wave partial counts per segment, flushed when the wave moves to another segment
+    uint32_t* red = reinterpret_cast<uint32_t*>(lds_all + wpb * per_wave + N);
+    if (a.count && lane < 2 * kMaxSeg) red[wave * 2 * kMaxSeg + lane] = 0u;
+    const int64_t segC = a.B * C;  // float4s per segment
 
     // prefetch registers: chunk q of tile t for this lane = float4 index t*64*C + lane + 64*q
     f4 nx[C];
-    int64_t pend_row0 = 0;  // previous tile: its msg_hat stores are issued one iteration late, before the
-    int pend_rows = 0;      // next prefetch, so the wait for that prefetch never waits for fresh stores
-    int64_t t = (int64_t)blockIdx.x * wpb + wave;
+    int64_t pend_row0 = 0;  // previous tile: its msg_hat stores are issued one iteration late
+    int pend_rows = 0, pend_seg = 0;
+    // position (seg, t) of this wave's tiles: global tile index g = seg * ntiles + t, stride gstride
     int64_t gstride = (int64_t)gridDim.x * wpb;
     asm volatile("" : "+s"(gstride));  // keep the grid stride in SGPRs (otherwise re-read every tile)
-    if (NPD_SCF_PREFETCH && t < a.ntiles) load_tile<C>(nx, y4, t, lane, a.B, last4);
+    const int64_t total = a.ntiles * a.n_seg;
+    int64_t g = (int64_t)blockIdx.x * wpb + wave;
+    int seg = (int)(g / (a.ntiles > 0 ? a.ntiles : 1));
+    int64_t t = g - (int64_t)seg * a.ntiles;
+    int cur_seg = seg;
+    if (NPD_SCF_PREFETCH && g < total)
+        load_tile<C>(nx, reinterpret_cast<const f4*>(a.y) + seg * segC, t, lane, a.B, segC - 1);
     unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0;
     unsigned long long ph[5] = {0, 0, 0, 0, 0};
-    for (; t < a.ntiles; t += gstride) {
+    auto flush = [&](int sg) {
+        const uint32_t eb = wave_sum_u32(err_bits);
+        const uint32_t bl = wave_sum_u32(err_blocks);
+        if (lane == 0) {
+            red[wave * 2 * kMaxSeg + 2 * sg] += eb;
+            red[wave * 2 * kMaxSeg + 2 * sg + 1] += bl;
+        }
+        err_bits = 0;
+        err_blocks = 0;
+    };
+    for (; g < total; g += gstride) {
         STAMP(ts0);
+        if (a.count && seg != cur_seg) {
+            flush(cur_seg);
+            cur_seg = seg;
+        }
+        float scale = a.scale[seg];
+        asm volatile("" : "+s"(scale));
+        const f4* y4 = reinterpret_cast<const f4*>(a.y) + seg * segC;
+        const int64_t last4 = segC - 1;  // last valid float4 of this segment
+        // next tile of this wave
+        int64_t tn = t + gstride;
+        int segn = seg;
+        while (tn >= a.ntiles && segn < a.n_seg) {
+            tn -= a.ntiles;
+            ++segn;
+        }
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
         // ---- this tile's message bits (Philox, pure VALU) first: it fills the wait for the tile's data.
@@ -458,20 +512,21 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
             }
         }
         // ---- prefetch the next tile as soon as its registers are free (lands while this one is decoded)
-        if (NPD_SCF_PREFETCH && NPD_SCF_ABL != 2 && t + gstride < a.ntiles)
-            load_tile<C>(nx, y4, t + gstride, lane, a.B, last4);
+        if (NPD_SCF_PREFETCH && NPD_SCF_ABL != 2 && g + gstride < total)
+            load_tile<C>(nx, reinterpret_cast<const f4*>(a.y) + segn * segC, tn, lane, a.B, last4);
         STAMP(ts2);
         // ---- previous tile's msg_hat (its decision rows are read before this tile's leaves overwrite them;
         // done before this tile's LLRs occupy registers)
-        if (NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4 && a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane, NB);
+        if (NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4 && a.msg && pend_rows > 0)
+            store_msg<N>(lds, kU, a.msg + pend_seg * a.B * K, pend_row0, pend_rows, K, lane, NB);
         if (!NPD_SCF_ROOT_LDS && NPD_SCF_ABL < 4) {
 #pragma unroll
             for (int q = 0; q < C; ++q) {
                 const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
-                c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
-                c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
-                c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
-                c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+                c.lv[N + 4 * q + 0] = rmul(scale, v.x);
+                c.lv[N + 4 * q + 1] = rmul(scale, v.y);
+                c.lv[N + 4 * q + 2] = rmul(scale, v.z);
+                c.lv[N + 4 * q + 3] = rmul(scale, v.w);
             }
         }
         }
@@ -504,17 +559,17 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
 #pragma unroll
                 for (int q = 0; q < C; ++q) {
                     const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
-                    c.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
-                    c.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
-                    c.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
-                    c.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+                    c.lv[N + 4 * q + 0] = rmul(scale, v.x);
+                    c.lv[N + 4 * q + 1] = rmul(scale, v.y);
+                    c.lv[N + 4 * q + 2] = rmul(scale, v.z);
+                    c.lv[N + 4 * q + 3] = rmul(scale, v.w);
                 }
                 c.slot = 0;
                 frozen_words();
                 node<N, n, 0>(c, p);
             }
         } else if (NPD_SCF_ROOT_LDS) {
-            root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, a.scale);
+            root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, scale);
         } else {
             node<N, n, 0>(c, p);
         }
@@ -553,6 +608,9 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
         ph[4] += ts5 - ts4;  // error count
         pend_row0 = row0;
         pend_rows = rows;
+        pend_seg = seg;
+        seg = segn;
+        t = tn;
     }
 #ifdef NPD_SCF_STAMPS
     if (lane == 0 && a.counters) {
@@ -561,27 +619,17 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
     }
 #endif
     // the last tile's msg_hat
-    if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg, pend_row0, pend_rows, K, lane, NB);
+    if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg + pend_seg * a.B * K, pend_row0, pend_rows, K, lane, NB);
 
     if (a.count && NPD_SCF_ABL != 5) {
-        // one pair of device atomics per workgroup: same-address atomics from every wave serialise at
-        // the memory side and cost ~20 us per launch
-        const uint32_t eb = wave_sum_u32(err_bits);
-        const uint32_t bl = wave_sum_u32(err_blocks);
-        uint32_t* red = reinterpret_cast<uint32_t*>(lds_all + wpb * per_wave + N);
-        if (lane == 0) {
-            red[2 * wave] = eb;
-            red[2 * wave + 1] = bl;
-        }
+        // one pair of device atomics per workgroup and segment: same-address atomics from every wave
+        // serialise at the memory side (~20 us per launch at one pair per wave)
+        flush(cur_seg);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long se = 0, sb = 0;
-            for (int w = 0; w < wpb; ++w) {
-                se += red[2 * w];
-                sb += red[2 * w + 1];
-            }
-            atomicAdd(a.counters + 0, se);
-            atomicAdd(a.counters + 1, sb);
+        if ((int)threadIdx.x < 2 * a.n_seg) {
+            unsigned long long sum = 0;
+            for (int w = 0; w < wpb; ++w) sum += red[w * 2 * kMaxSeg + threadIdx.x];
+            if (sum) atomicAdd(a.counters + threadIdx.x, sum);
         }
     }
 }
@@ -593,8 +641,9 @@ static int launch(const CodeParams& p, Args a, hipStream_t s) {
     const size_t per_wave = (size_t)kWave * N * 4 + (size_t)kWave * NB;
     // as many waves per workgroup as fit (up to NPD_SCF_WPB): fewer workgroups -> fewer counter atomics
     int wpb = NPD_SCF_WPB;
-    while (wpb > 1 && (size_t)wpb * per_wave + N + 8 * wpb > 160 * 1024) --wpb;
-    const size_t lds = (size_t)wpb * per_wave + N + 8 * wpb;
+    const size_t red = (size_t)8 * kMaxSeg;  // per wave: n_seg x {bits, blocks} uint32
+    while (wpb > 1 && (size_t)wpb * (per_wave + red) + N > 160 * 1024) --wpb;
+    const size_t lds = (size_t)wpb * (per_wave + red) + N;
     a.ntiles = (a.B + kWave - 1) / kWave;
     auto kern = sc_fast_kernel<N, MASK, SPEC>;
     static bool attr = false;
@@ -607,7 +656,7 @@ static int launch(const CodeParams& p, Args a, hipStream_t s) {
         (void)hipGetLastError();
         occ = 1;
     }
-    const int64_t groups = (a.ntiles + wpb - 1) / wpb;
+    const int64_t groups = (a.ntiles * a.n_seg + wpb - 1) / wpb;
     const int grid = grid_for(groups, occ, device_cu_count());
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave * wpb), lds, s, p, a);
     return launch_check("sc_fast_kernel launch");
@@ -631,8 +680,9 @@ bool sc_fast_eligible(const CodeParams& p, const void* y) {
     return !p.pac && p.N >= 8 && p.N <= 64 && p.K <= 128 && (((uintptr_t)y) & 15) == 0;
 }
 
-int sc_fast_run(const CodeParams& p, const float* y, float llr_scale, float* msg, unsigned long long* counters,
-                uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s) {
+int sc_fast_run(const CodeParams& p, const float* y, const float* llr_scale, int n_seg, float* msg,
+                unsigned long long* counters, uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s) {
+    if (n_seg < 1 || n_seg > scf::kMaxSeg) return fail(NPD_EINVAL, "sc_fast: 1 <= segments <= 16");
     scf::Args a{};
     a.y = y;
     a.msg = msg;
@@ -640,7 +690,8 @@ int sc_fast_run(const CodeParams& p, const float* y, float llr_scale, float* msg
     a.seed = seed;
     a.cw_offset = cw_offset;
     a.B = B;
-    a.scale = llr_scale;
+    a.n_seg = n_seg;
+    for (int i = 0; i < n_seg; ++i) a.scale[i] = llr_scale[i];
     a.count = counters ? 1u : 0u;
     // the reference's standard codes ('polar' rate profile, K = N/2) have specialised decoders
     if (!spec_disabled() && p.N <= 64) {

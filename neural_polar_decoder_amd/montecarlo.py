@@ -84,13 +84,17 @@ class MonteCarlo:
     def count_batch(self, si, snr, cw_offset, n, counters_row):  # pragma: no cover - abstract
         raise NotImplementedError
 
+    def count_sweep(self, cw_offset, n, counters):
+        """All SNR points of one batch; the default runs count_batch per SNR."""
+        for si, snr in enumerate(self.snrs):
+            self.count_batch(si, snr, cw_offset, n, counters[si])
+
     def run(self) -> MCResult:
         start, count = shard_range(self.total, self.rank, self.world)
         counters = self.new_counters()
         for off in range(0, count, self.batch):
             n = min(self.batch, count - off)
-            for si, snr in enumerate(self.snrs):
-                self.count_batch(si, snr, start + off, n, counters[si])
+            self.count_sweep(start + off, n, counters)
         d = _dist()
         if d is not None and self.world > 1:
             d.all_reduce(counters)  # the one collective of the run
@@ -111,6 +115,17 @@ class SCMonteCarlo(MonteCarlo):
         _, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=False)
         self.code.sc_decode_mc(y, snr, self.seed, cw_offset, counters_row)
 
+    def count_sweep(self, cw_offset, n, counters):
+        if not hasattr(self.code, "sc_decode_mc_sweep") or len(self.snrs) > 16:
+            return super().count_sweep(cw_offset, n, counters)
+        # Polar: every SNR point of the batch in one decode launch (npd_sc_decode_mc_sweep)
+        if self._y is None or self._y.shape[1] != n:
+            self._y = torch.empty(len(self.snrs), n, self.code.N, dtype=torch.float32, device=self.device)
+        y = self._y
+        for si, snr in enumerate(self.snrs):
+            self.code.mc_generate(n, snr, self.seed, si, cw_offset, want_msg=False, out=y[si])
+        self.code.sc_decode_mc_sweep(y, self.snrs, self.seed, cw_offset, counters)
+
 
 class SCLMonteCarlo(SCMonteCarlo):
     """Polar SC-List decoding (polar.py:793-876, run_models.py:327-331): fused generate +
@@ -123,6 +138,9 @@ class SCLMonteCarlo(SCMonteCarlo):
     def count_batch(self, si, snr, cw_offset, n, counters_row):
         _, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=False)
         self.code.scl_decode_mc(y, snr, self.list_size, self.seed, cw_offset, counters_row)
+
+    def count_sweep(self, cw_offset, n, counters):
+        return MonteCarlo.count_sweep(self, cw_offset, n, counters)
 
 
 class GRUMonteCarlo(MonteCarlo):

@@ -199,15 +199,29 @@ class PolarCode:
     # the eval loops do not call; out of scope here.
 
     # ------------------------------------------------------------------ Monte-Carlo extras
-    def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False):
-        device = torch.device(device or "cuda")
-        y = torch.empty(B, self.N, dtype=torch.float32, device=device)
+    def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False, out=None):
+        device = torch.device(device or "cuda") if out is None else out.device
+        y = torch.empty(B, self.N, dtype=torch.float32, device=device) if out is None else out
         msg = torch.empty(B, self.K, dtype=torch.float32, device=device) if want_msg else None
         x = torch.empty(B, self.N, dtype=torch.float32, device=device) if want_x else None
         _lib.check(_lib.load().npd_mc_generate(self.code.h, _lib.ptr(msg), _lib.ptr(x), _lib.ptr(y), B, sigma_f32(snr),
                                                int(seed), int(snr_index), int(cw_offset), _lib.stream_of(device)),
                    "npd_mc_generate")
         return msg, x, y
+
+    def sc_decode_mc_sweep(self, y, snrs, seed, cw_offset, counters, msg_hat=None):
+        """y (n_snr, B, N) -> counters (n_snr, 2) += errors at each SNR, one launch (npd_sc_decode_mc_sweep)."""
+        _lib.require_gpu(y, "y")
+        n, B = y.shape[0], y.shape[1]
+        scales = np.asarray([llr_scale(s) for s in snrs], dtype=np.float32)
+        if len(scales) != n:
+            raise ValueError("one SNR per y segment")
+        y = _lib.f32c(y)
+        _lib.check(_lib.load().npd_sc_decode_mc_sweep(self.code.h, n, _lib.ptr(y), scales.ctypes.data_as(ctypes.c_void_p),
+                                                      _lib.ptr(msg_hat), int(seed), int(cw_offset), B,
+                                                      _lib.ptr(counters), _lib.stream_of(y.device)),
+                   "npd_sc_decode_mc_sweep")
+        return counters
 
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")

@@ -285,3 +285,29 @@ def test_specialised_8_4_and_high_snr_vs_oracle(oracle):
             _, _, y = code.mc_generate(20000, snr, seed=4, want_msg=False)
             _, oh = oracle.sc_decode(y.cpu().numpy(), snr, code.info_positions)
             assert np.array_equal(code.sc_decode_msg(y, snr).cpu().numpy(), oh), (N, snr)
+
+
+@pytest.mark.parametrize("N,K,B", [(64, 32, 100_003), (32, 16, 5000), (16, 8, 777), (64, 22, 3001)])
+def test_sweep_equals_per_snr_calls(N, K, B):
+    """npd_sc_decode_mc_sweep (one launch over all SNR points) == separate npd_sc_decode_mc calls:
+    same msg_hat bits and counters at every SNR, ragged B, specialised and generic codes."""
+    from neural_polar_decoder_amd import PolarCode, reference_polar_code
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    if K == 22:
+        info = polar_info_positions(N, K)
+        code = PolarCode(int(np.log2(N)), K, F=np.setdiff1d(np.arange(N), info))
+    else:
+        code = reference_polar_code(N, K)
+    snrs = [0.0, 1.5, 3.0, 5.0]
+    y = torch.empty(len(snrs), B, N, device=DEV)
+    for i, s in enumerate(snrs):
+        code.mc_generate(B, s, 11, i, 7, out=y[i], want_msg=False)
+    c1 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    h1 = torch.empty(len(snrs), B, K, device=DEV)
+    code.sc_decode_mc_sweep(y, snrs, 11, 7, c1, msg_hat=h1)
+    c2 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    for i, s in enumerate(snrs):
+        h = torch.empty(B, K, device=DEV)
+        code.sc_decode_mc(y[i], s, 11, 7, c2[i], msg_hat=h)
+        assert torch.equal(h, h1[i]), s
+    assert torch.equal(c1, c2)
