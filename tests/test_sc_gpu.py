@@ -260,7 +260,7 @@ def test_montecarlo_pac_and_gru_drivers_run():
     assert all(0.3 < b < 0.7 for b in g.ber)  # untrained weights: coin flips
 
 
-@pytest.mark.parametrize("N,K", [(64, 32), (32, 16), (16, 8)])
+@pytest.mark.parametrize("N,K", [(64, 32), (32, 16), (16, 8), (64, 22)])
 def test_msg_only_fast_paths_on_golden_including_crafted_rows(N, K):
     """msg-only decoding takes the streaming kernels (for these standard codes the frozen-set-specialised
     one, whose closed-form subtrees fall back to step-by-step SC on huge or zero LLRs): same msg_hat as
