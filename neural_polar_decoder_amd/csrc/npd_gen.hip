@@ -84,8 +84,10 @@ __global__ __launch_bounds__(256) void awgn_kernel(const float4* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------- fused MC generation
-// One lane per codeword: Philox message bits -> positions (bit domain) -> PAC conv (bit domain) ->
-// Plotkin butterfly as XOR on 32-bit words -> BPSK -> + sigma * N(0,1).
+// Phase 1, one lane per codeword: Philox message bits -> positions (bit domain) -> PAC conv (bit domain) ->
+// Plotkin butterfly as XOR on 32-bit words; the codeword's bits go to LDS.  Phase 2, one lane per 16-B
+// chunk of the wave's 64 x N output tile: BPSK + sigma * N(0,1) (Philox counter = (chunk, codeword), so
+// the mapping of work to lanes does not change any value), stored coalesced.
 template <int N>
 __global__ __launch_bounds__(256) void mc_generate_kernel(const CodeParams p, float* __restrict__ msg,
                                                           float* __restrict__ x, float* __restrict__ y, int64_t B,
@@ -93,89 +95,106 @@ __global__ __launch_bounds__(256) void mc_generate_kernel(const CodeParams p, fl
                                                           uint64_t cw_offset) {
     constexpr int NW = (N + 31) / 32;
     constexpr int MB = (N + 127) / 128;  // Philox blocks for up to N message bits
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    const uint64_t cw = cw_offset + (uint64_t)b;
-    uint32_t m[4 * MB];
+    constexpr int C = N / 4;             // 16-B chunks per row
+    __shared__ uint32_t sU[4][kWave][NW];
+    __shared__ uint32_t sM[4][kWave][4 * MB + 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t b0 = ((int64_t)blockIdx.x * 4 + wave) * kWave;
+    const int64_t b = b0 + lane;
+    if (b < B) {
+        const uint64_t cw = cw_offset + (uint64_t)b;
+        uint32_t m[4 * MB];
 #pragma unroll
-    for (int blk = 0; blk < MB; ++blk) {
-        const u32x4 o = philox_block(seed, kStreamMsg, cw, (uint32_t)blk);
-        m[4 * blk + 0] = o.x; m[4 * blk + 1] = o.y; m[4 * blk + 2] = o.z; m[4 * blk + 3] = o.w;
-    }
-    if (msg) {
-        for (int k = 0; k < p.K; ++k) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int q = 0; q < 4 * MB; ++q) w = ((k >> 5) == q) ? m[q] : w;
-            msg[b * p.K + k] = ((w >> (k & 31)) & 1u) ? -1.0f : 1.0f;
+        for (int blk = 0; blk < MB; ++blk) {
+            const u32x4 o = philox_block(seed, kStreamMsg, cw, (uint32_t)blk);
+            m[4 * blk + 0] = o.x; m[4 * blk + 1] = o.y; m[4 * blk + 2] = o.z; m[4 * blk + 3] = o.w;
         }
-    }
-    // scatter message bits to positions: info positions are sorted, so slot k advances with i
-    uint32_t U[NW];
+        if (msg) {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) U[w] = 0;
-    uint32_t cur = m[0];
-    int kk = 0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        if (!((p.frozen[i >> 5] >> (i & 31)) & 1u)) {
-            U[i >> 5] |= (cur & 1u) << (i & 31);
-            cur >>= 1;
-            ++kk;
-            if ((kk & 31) == 0) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int q = 1; q < 4 * MB; ++q) w = ((kk >> 5) == q) ? m[q] : w;
-                cur = w;
-            }
+            for (int q = 0; q < 4 * MB; ++q) sM[wave][lane][q] = m[q];
         }
-    }
-    if (p.pac) {
-        // u_i = v_i xor parity(state & taps); state <- v (pac_code.py:181-208), bit domain (1 == -1)
-        uint32_t st = 0;
+        // scatter message bits to positions: info positions are sorted, so slot k advances with i
+        uint32_t U[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) U[w] = 0;
+        uint32_t cur = m[0];
+        int kk = 0;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            const uint32_t v = (U[i >> 5] >> (i & 31)) & 1u;
-            const uint32_t par = (uint32_t)__builtin_popcount(st & p.tapmask) & 1u;
-            U[i >> 5] ^= par << (i & 31);
-            st = ((st << 1) | v) & p.smask;
+            if (!((p.frozen[i >> 5] >> (i & 31)) & 1u)) {
+                U[i >> 5] |= (cur & 1u) << (i & 31);
+                cur >>= 1;
+                ++kk;
+                if ((kk & 31) == 0) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int q = 1; q < 4 * MB; ++q) w = ((kk >> 5) == q) ? m[q] : w;
+                    cur = w;
+                }
+            }
+        }
+        if (p.pac) {
+            // u_i = v_i xor parity(state & taps); state <- v (pac_code.py:181-208), bit domain (1 == -1)
+            uint32_t st = 0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const uint32_t v = (U[i >> 5] >> (i & 31)) & 1u;
+                const uint32_t par = (uint32_t)__builtin_popcount(st & p.tapmask) & 1u;
+                U[i >> 5] ^= par << (i & 31);
+                st = ((st << 1) | v) & p.smask;
+            }
+        }
+        // Plotkin butterfly: left ^= right, stage order irrelevant in GF(2)
+#pragma unroll
+        for (int h = 1; h < 32 && h < N; h <<= 1) {
+            uint32_t msk = 0;
+            for (int i = 0; i < 32; ++i)
+                if (((i / h) & 1) == 0) msk |= 1u << i;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) U[w] ^= (U[w] >> h) & msk;
+        }
+#pragma unroll
+        for (int hw = 1; hw < NW; hw <<= 1)
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (((w / hw) & 1) == 0) U[w] ^= U[w + hw];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) sU[wave][lane][w] = U[w];
+    }
+    __syncthreads();
+    if (msg) {  // message rows of the tile, coalesced: float f = codeword f / K, bit f % K
+        const int64_t nf = (B - b0 < kWave ? B - b0 : kWave) * (int64_t)p.K;
+        float* mt = msg + b0 * p.K;
+        for (int f = lane; f < nf; f += kWave) {
+            const int r = f / p.K, k = f % p.K;
+            mt[f] = ((sM[wave][r][k >> 5] >> (k & 31)) & 1u) ? -1.0f : 1.0f;
         }
     }
-    // Plotkin butterfly: left ^= right, stage order irrelevant in GF(2)
+    // BPSK + noise, coalesced: chunk g of the tile = codeword g / C, float4 g % C of its row
+    float4* yt = reinterpret_cast<float4*>(y) + b0 * C;
+    float4* xt = x ? reinterpret_cast<float4*>(x) + b0 * C : nullptr;
+    const int64_t nchunks = (B - b0 < kWave ? B - b0 : kWave) * C;
+#pragma unroll 4
+    for (int q = 0; q < C; ++q) {
+        const int g = lane + kWave * q;
+        if (g < nchunks) {
+            const int r = g / C, j = g % C;
+            const uint64_t cw = cw_offset + (uint64_t)(b0 + r);
+            const u32x4 o = philox_block(seed, kStreamNoise + snr_index, cw, (uint32_t)j);
+            float z[4];
+            normals4(o, z);
+            const uint32_t bits = (sU[wave][r][(4 * j) >> 5] >> ((4 * j) & 31)) & 0xFu;
+            float xv[4];
 #pragma unroll
-    for (int h = 1; h < 32 && h < N; h <<= 1) {
-        uint32_t msk = 0;
-        for (int i = 0; i < 32; ++i)
-            if (((i / h) & 1) == 0) msk |= 1u << i;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) U[w] ^= (U[w] >> h) & msk;
-    }
-#pragma unroll
-    for (int hw = 1; hw < NW; hw <<= 1)
-#pragma unroll
-        for (int w = 0; w < NW; ++w)
-            if (((w / hw) & 1) == 0) U[w] ^= U[w + hw];
-    // BPSK + noise; 16-B stores of the lane's own row
-    float4* yr = reinterpret_cast<float4*>(y + b * N);
-    float4* xr = x ? reinterpret_cast<float4*>(x + b * N) : nullptr;
-#pragma unroll
-    for (int j = 0; j < N / 4; ++j) {
-        const u32x4 o = philox_block(seed, kStreamNoise + snr_index, cw, (uint32_t)j);
-        float z[4];
-        normals4(o, z);
-        float xv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int i = 4 * j + e;
-            xv[e] = ((U[i >> 5] >> (i & 31)) & 1u) ? -1.0f : 1.0f;
+            for (int e = 0; e < 4; ++e) xv[e] = ((bits >> e) & 1u) ? -1.0f : 1.0f;
+            float4 yv;
+            yv.x = __fadd_rn(xv[0], __fmul_rn(sigma, z[0]));
+            yv.y = __fadd_rn(xv[1], __fmul_rn(sigma, z[1]));
+            yv.z = __fadd_rn(xv[2], __fmul_rn(sigma, z[2]));
+            yv.w = __fadd_rn(xv[3], __fmul_rn(sigma, z[3]));
+            yt[g] = yv;
+            if (xt) xt[g] = make_float4(xv[0], xv[1], xv[2], xv[3]);
         }
-        float4 yv;
-        yv.x = __fadd_rn(xv[0], __fmul_rn(sigma, z[0]));
-        yv.y = __fadd_rn(xv[1], __fmul_rn(sigma, z[1]));
-        yv.z = __fadd_rn(xv[2], __fmul_rn(sigma, z[2]));
-        yv.w = __fadd_rn(xv[3], __fmul_rn(sigma, z[3]));
-        yr[j] = yv;
-        if (xr) xr[j] = make_float4(xv[0], xv[1], xv[2], xv[3]);
     }
 }
 
@@ -238,7 +257,7 @@ extern "C" int npd_awgn(const float* x, float* y, int64_t B, int N, float sigma,
 template <int N>
 static int mc_gen_launch(const npd_code* code, float* msg, float* x, float* y, int64_t B, float sigma, uint64_t seed,
                          uint32_t snr_index, uint64_t cw_offset, hipStream_t s) {
-    const int64_t blocks = (B + 255) / 256;
+    const int64_t blocks = (B + 4 * kWave - 1) / (4 * kWave);
     hipLaunchKernelGGL(gen::mc_generate_kernel<N>, dim3((unsigned)blocks), dim3(256), 0, s, code->p, msg, x, y, B, sigma,
                        seed, snr_index, cw_offset);
     return launch_check("mc_generate_kernel launch");
