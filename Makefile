@@ -31,11 +31,12 @@ $(LIB): $(OBJS)
 
 # Oracle: plain C, no fast-math, no FMA contraction (exact restatement of the reference's fp32 ops).
 # The SCL restatement is C++ so that list pruning calls libstdc++'s std::nth_element (torch.topk's CPU path).
-$(ORACLE): oracle/npd_oracle.c oracle/npd_oracle_scl.cpp
+$(ORACLE): oracle/npd_oracle.c oracle/npd_oracle_scl.cpp oracle/npd_oracle_lse.c
 	@mkdir -p build/oracle
 	gcc -O2 -std=c11 -fPIC -fopenmp -ffp-contract=off -c oracle/npd_oracle.c -o build/oracle/npd_oracle.o
 	g++ -O2 -std=c++17 -fPIC -fopenmp -ffp-contract=off -c oracle/npd_oracle_scl.cpp -o build/oracle/npd_oracle_scl.o
-	g++ -shared -fopenmp -o $@ build/oracle/npd_oracle.o build/oracle/npd_oracle_scl.o -lm
+	gcc -O2 -std=c11 -fPIC -fopenmp -ffp-contract=off -c oracle/npd_oracle_lse.c -o build/oracle/npd_oracle_lse.o
+	g++ -shared -fopenmp -o $@ build/oracle/npd_oracle.o build/oracle/npd_oracle_scl.o build/oracle/npd_oracle_lse.o -lm
 
 asm: $(CSRC)
 	@mkdir -p build/asm

@@ -2,7 +2,7 @@
 """Headline benchmark: Polar(64,32) SC decoding on MI355X (BASELINE.json configs[1]).
 
 One "step" = SC-decode one batch of B = 2^20 received words per SNR point for the SNR sweep
-0,1,2,3,4 dB (5 launches of the fused decode + BER/BLER-count kernel; y already resident in HBM,
+0,1,2,3,4 dB (one launch of the fused decode + BER/BLER-count kernel; y already resident in HBM,
 msg_hat (B,K) fp32 written back, error counters accumulated on device).
 
   python bench.py [--gpus N --steps K --warmup W]
@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--no-conv", action="store_true", help="skip the secondary conv-model measurement")
     ap.add_argument("--no-scl", action="store_true", help="skip the secondary SC-List measurement")
+    ap.add_argument("--no-lse", action="store_true", help="skip the secondary exact-LSE SC measurement")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -176,6 +177,28 @@ def scl_measure(code, dev, y, snr, batch=1 << 18, iters=3):
             "avg_launch_ms": res["L4"]["avg_launch_ms"], "L8": res["L8"],
             "bound": "VALU/LDS (per-path SC + list bookkeeping; 384 B/cw of HBM traffic is not the limit)",
             "config": "Polar(64,32) scl_decode(L) (polar.py:793-876), 2 dB, decode + fused BER/BLER counts"}
+
+
+def lse_measure(code, dev, y, snr, batch=1 << 18, iters=2):
+    """Secondary line: exact-LSE SC (PolarCode.sc_decode, polar.py:209-279),
+    Polar(64,32) at 2 dB, hard and soft decisions, msg_hat out.  Transcendental-bound (4 exp/log per
+    check node, 192 check nodes per codeword)."""
+    yb = y[:batch].contiguous()
+    res = {}
+    for tag, hard in (("hard", True), ("soft", False)):
+        code.sc_decode(yb, snr, hard_decision=hard)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            code.sc_decode(yb, snr, hard_decision=hard)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        res[tag] = {"value": batch / (ms / 1e3), "avg_launch_ms": ms}
+    return {"value": res["soft"]["value"], "unit": "codewords/s", "batch": batch, "soft": res["soft"],
+            "hard": res["hard"], "bound": "transcendental VALU (exp/log per check node)",
+            "config": "Polar(64,32) sc_decode exact-LSE (polar.py:209-279), 2 dB, msg_hat out"}
 
 
 def conv_measure(dev, batch=8192, iters=3):
@@ -349,6 +372,8 @@ def main():
         out["crisp_gru"] = gru_measure(code, dev, ys[2], snrs[2])
     if not args.no_scl:
         out["scl"] = scl_measure(code, dev, ys[2], snrs[2])
+    if not args.no_lse:
+        out["sc_lse"] = lse_measure(code, dev, ys[2], snrs[2])
     if not args.no_conv:
         out["conv_model"] = conv_measure(dev)
     if not args.no_traffic and world == 1:

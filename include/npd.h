@@ -107,6 +107,17 @@ int npd_sc_decode(const npd_code* code, const float* y, float llr_scale, float* 
 int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_scale, float* msg_hat, uint64_t seed,
                      uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream);
 
+/*
+ * Exact log-sum-exp SC, PolarCode.sc_decode(noisy_code, snr) (polar.py:209-279): check node =
+ * log_sum_avoid_zero_NaN (utils.py:295-397), g = u*a + b, frozen leaves decided +1 (no prior),
+ * information leaves sign(L) (hard_decision != 0, args.hard_decision) or tanh(L/2) (hard_decision == 0,
+ * the reference's default).  Outputs (each optional): msg_hat = sign(decoded_bits)[:, info] (B,K) and
+ * u_bits = decoded_bits (B,N).  Polar codes, N <= 256.  exp/log/tanh are the device libm, so values
+ * agree with torch's CPU path to a few ulp (decisions except on near-zero LLRs).
+ */
+int npd_sc_decode_lse(const npd_code* code, const float* y, float llr_scale, int hard_decision, float* msg_hat,
+                      float* u_bits, int64_t B, void* stream);
+
 /* ---------------------------------------------------------------------------------- SC-List decode */
 /*
  * Successive-cancellation list decoding, PolarCode.scl_decode(y, snr, L, use_CRC=False)

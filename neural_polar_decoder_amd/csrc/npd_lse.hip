@@ -1,0 +1,193 @@
+// npd_lse.hip -- exact log-sum-exp successive-cancellation decoding for gfx950.
+//
+// Replaces PolarCode.sc_decode / decode (polar.py:209-279): the same SC tree as sc_decode_new, but
+//   * the check-node update is the exact boxplus of utils.py:348-397 (log_sum_avoid_zero_NaN), not
+//     min-sum;
+//   * frozen leaves are decided +1 outright (no LLR prior, polar.py:236-238, 249-251);
+//   * information leaves decide sign(L) (args.hard_decision) or tanh(L/2) (the reference's argparse
+//     default, "soft SC"), and the partial sums propagated up the tree are products of those values;
+//   * the output is sign(decoded_bits)[:, info] (polar.py:222), optionally decoded_bits itself.
+//
+// This decoder is transcendental-bound (4 exp/log per check node), not HBM-bound, so the design is the
+// simple one: one codeword per lane, the SC schedule walked iteratively (leaf i: one g step at depth
+// ctz(i)+1, f steps down to the leaf, partial-sum combines for the ctz(i+1) finished nodes), and the
+// per-lane LLR levels (N-1 floats) and partial sums (N floats) in LDS, lane-interleaved
+// (element e of lane l at dword e*64 + l: every access of a wave is conflict-free).  The root level is
+// read from y directly (two passes: f then g), through L1/L2.
+//
+// Floating point: each reference tensor op is one rounded fp32 op here (no contraction: rmul makes
+// every product opaque); exp/log/tanh are the device libm (<= 1 ulp, as is torch's CPU Sleef path),
+// so results agree with the reference to a few ulp and decisions agree except on near-zero LLRs
+// (tests/test_lse_gpu.py states the tolerance).
+#include "npd_common.hpp"
+
+namespace npd {
+namespace lse {
+
+struct Args {
+    const float* y;
+    float* msg;     // (B,K) sign(decoded_bits)[:, info], or null
+    float* ubits;   // (B,N) decoded_bits, or null
+    int64_t B;
+    int64_t ntiles;
+    float scale;
+};
+
+__device__ __forceinline__ float rmul(float a, float b) {
+    float r = a * b;
+    asm("" : "+v"(r));
+    return r;
+}
+
+// log_sum_avoid_NaN (utils.py:295-345) evaluated elementwise.  The reference computes the "standard"
+// formula and, only if the TENSOR holds a NaN/inf, patches four index sets.  Every element of a patched
+// set either has a non-finite standard value (so the patch always runs for it) or a patched value equal
+// to its standard value bit for bit, so applying the patches per element unconditionally is exact.
+__device__ __forceinline__ float lse_avoid_nan(float x, float y) {
+    const float s = x + y;
+    const float dyx = y - x;
+    const float t1 = logf(1.0f + expf(s));    // torch.log(1 + (x+y).exp())
+    const float t3 = logf(1.0f + expf(dyx));  // torch.log(1 + (y-x).exp())
+    float r = (t1 - x) - t3;
+    const float ad = fabsf(x - y);
+    const float mx = (x > y) ? x : y;  // a = torch.max(x, y)  (x, y are not NaN on these branches)
+    const float mn = (x < y) ? x : y;  // b = torch.min(x, y)
+    if (s > 200.0f) {                         // idx_1
+        r = (ad < 200.0f) ? (y - t3) : mn;    // subset_1 / idx_1 ^ subset_1
+    } else if (s < -200.0f) {                 // idx_2
+        r = (ad < 200.0f) ? (-x - t3) : -mx;  // subset_2 / idx_2 ^ subset_2
+    } else if (ad > 200.0f && fabsf(s) < 200.0f) {
+        r = t1 - mx;                          // idx_3
+    }
+    return r;
+}
+
+// log_sum_avoid_zero_NaN (utils.py:348-397): re-evaluate exact zeros with the shifted formula
+__device__ __forceinline__ float lse_f(float x, float y) {
+    float r = lse_avoid_nan(x, y);
+    if (r == 0.0f) {
+        const float s = x + y;
+        const float nume = (s < 0.0f) ? 0.0f : s;  // torch.relu (keeps -0)
+        const float denom = (x > y) ? x : y;       // torch.max
+        const float term1 = 0.5f * (expf(-nume) + expf(s - nume));
+        const float term2 = 0.5f * (expf(x - denom) + expf(y - denom));
+        const float T1 = (fabsf(term1 - 1.0f) < 1e-7f) ? (term1 - 1.0f) : logf(term1);
+        const float T2 = (fabsf(term2 - 1.0f) < 1e-7f) ? (term2 - 1.0f) : logf(term2);
+        float c = ((nume - denom) + T1) - T2;
+        if (c == 0.0f) {
+            const float a = (x < y) ? x : y;      // torch.min(x, y)
+            const float b = (-x < -y) ? -x : -y;  // torch.min(-x, -y)
+            c = (s > 0.0f) ? a : b;
+        }
+        r = c;
+    }
+    return r;
+}
+
+// g = u_hat * L_left + L_right (polar.py:253, 276); u is +-1/0 (hard) or a tanh product (soft)
+__device__ __forceinline__ float lse_g(float u, float a, float b) { return rmul(u, a) + b; }
+
+template <bool SOFT>
+__global__ __launch_bounds__(64) void lse_sc_kernel(const CodeParams p, const Args a) {
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x;
+    const int N = p.N, n = p.n, K = p.K;
+    float* const L = lds + lane;              // LLR level d (2^d values) at elements [2^d - 1, 2^(d+1) - 1)
+    float* const beta = L + (N - 1) * kWave;  // partial sums, N values
+#define LV(base, j) (L[((base) + (j)) * kWave])
+#define BT(j) (beta[(j) * kWave])
+
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t row = t * kWave + lane;
+        const bool valid = row < a.B;
+        const int64_t r = valid ? row : a.B - 1;
+        const float* yr = a.y + r * N;
+        float* ub = (a.ubits && valid) ? a.ubits + row * N : nullptr;
+        float* mh = (a.msg && valid) ? a.msg + row * K : nullptr;
+
+        for (int i = 0; i < N; ++i) {
+            int d;
+            if (i == 0) {  // left child of the root: f on the channel LLRs
+                const int h = N >> 1;
+                for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_f(rmul(a.scale, yr[j]), rmul(a.scale, yr[j + h]));
+                d = n - 1;
+            } else {  // right child of the node of 2^(k+1) leaves starting at i - 2^k
+                const int k = __builtin_ctz((unsigned)i);
+                const int h = 1 << k;
+                const int s = i - h;
+                if (k + 1 == n) {
+                    for (int j = 0; j < h; ++j)
+                        LV(h - 1, j) = lse_g(BT(s + j), rmul(a.scale, yr[j]), rmul(a.scale, yr[j + h]));
+                } else {
+                    for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_g(BT(s + j), LV(2 * h - 1, j), LV(2 * h - 1, j + h));
+                }
+                d = k;
+            }
+            for (int dd = d; dd >= 1; --dd) {  // left children down to the leaf
+                const int h = 1 << (dd - 1);
+                for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_f(LV(2 * h - 1, j), LV(2 * h - 1, j + h));
+            }
+            // leaf (polar.py:233-262)
+            const bool frozen = (p.frozen[i >> 5] >> (i & 31)) & 1u;
+            float u = 1.0f;
+            if (!frozen) {
+                const float Lf = LV(0, 0);
+                u = SOFT ? tanhf(Lf * 0.5f) : sgnf(Lf);
+            }
+            BT(i) = u;
+            if (ub) ub[i] = u;
+            if (mh && !frozen) mh[p.rank[i]] = sgnf(u);
+            // combine partial sums of every node whose right child ends at leaf i (polar.py:264, 279)
+            for (int l = 1; l < n && ((i + 1) & ((1 << l) - 1)) == 0; ++l) {
+                const int h = 1 << (l - 1);
+                const int s = i + 1 - (1 << l);
+                for (int j = 0; j < h; ++j) BT(s + j) = BT(s + j) * BT(s + h + j);
+            }
+        }
+    }
+#undef LV
+#undef BT
+}
+
+template <bool SOFT>
+static int launch(const CodeParams& p, Args a, hipStream_t stream) {
+    const size_t lds = (size_t)(2 * p.N - 1) * kWave * sizeof(float);
+    auto kern = lse_sc_kernel<SOFT>;
+    static bool attr_set = false;  // benign race (idempotent)
+    if (!attr_set && lds > 65536) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr_set = true;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    a.ntiles = (a.B + kWave - 1) / kWave;
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, stream, p, a);
+    return launch_check("lse_sc_kernel launch");
+}
+
+}  // namespace lse
+}  // namespace npd
+
+using namespace npd;
+
+extern "C" int npd_sc_decode_lse(const npd_code* code, const float* y, float llr_scale, int hard_decision,
+                                 float* msg_hat, float* u_bits, int64_t B, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_decode_lse: code is NULL");
+    NPD_ARG(!code->p.pac, "npd_sc_decode_lse: Polar codes only (PolarCode.sc_decode)");
+    NPD_ARG(code->p.N >= 2 && code->p.N <= kMaxN, "npd_sc_decode_lse: 2 <= N <= 256");
+    NPD_ARG(B >= 0, "npd_sc_decode_lse: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_lse: y is NULL");
+    if (B == 0) return NPD_OK;
+    lse::Args a{};
+    a.y = y;
+    a.msg = msg_hat;
+    a.ubits = u_bits;
+    a.B = B;
+    a.scale = llr_scale;
+    return hard_decision ? lse::launch<false>(code->p, a, (hipStream_t)stream)
+                         : lse::launch<true>(code->p, a, (hipStream_t)stream);
+}

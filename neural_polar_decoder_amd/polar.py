@@ -8,6 +8,7 @@ through libnpd (HIP kernels, ctypes C-ABI).  Tensors must live on the GPU.
   .encode  (alias of encode_plotkin, as rnn_all.get_code sets it, rnn_all.py:1187)
   .channel(code, snr)                                                           polar.py:201-207
   .sc_decode_new(corrupted_codewords, snr, use_gt=None) -> (leaf_llrs, msg_hat) polar.py:465-484
+  .sc_decode(noisy_code, snr) -> msg_hat   (exact-LSE SC, hard or soft)         polar.py:209-279
 
 MI355X extras (no reference equivalent, used by the Monte-Carlo driver and bench):
   .mc_generate(B, snr, seed, snr_index, cw_offset)   fused msg -> encode -> AWGN on device
@@ -195,8 +196,27 @@ class PolarCode:
                                                  _lib.stream_of(y.device)), "npd_scl_decode_mc")
         return counters
 
-    # The reference's ``sc_decode`` (polar.py:209-279) is a different (exact-LSE, soft) decoder that
-    # the eval loops do not call; out of scope here.
+    # ------------------------------------------------------------------ exact-LSE SC (polar.py:209-279)
+    def sc_decode(self, noisy_code, snr, hard_decision=None, return_bits=False):
+        """PolarCode.sc_decode: SC with the exact boxplus (log_sum_avoid_zero_NaN, utils.py:295-397), no
+        frozen prior; returns decoded_message = sign(decoded_bits)[:, info] (B,K).
+
+        Decisions follow ``self.args.hard_decision`` as in the reference (sign(L) if set, else the soft
+        tanh(L/2) -- argparse's default); ``hard_decision=`` overrides it.  ``return_bits=True`` also
+        returns decoded_bits (B,N).  Not the min-sum ``sc_decode_new`` the eval loops call."""
+        _lib.require_gpu(noisy_code, "noisy_code")
+        if hard_decision is None:
+            hard_decision = bool(getattr(self.args, "hard_decision", False)) if self.args is not None else False
+        y = _lib.f32c(noisy_code)
+        if y.dim() != 2 or y.shape[1] != self.N:
+            raise ValueError(f"noisy_code must be (batch, {self.N}), got {tuple(y.shape)}")
+        B = y.shape[0]
+        hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
+        bits = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_bits else None
+        _lib.check(_lib.load().npd_sc_decode_lse(self.code.h, _lib.ptr(y), llr_scale(snr), 1 if hard_decision else 0,
+                                                 _lib.ptr(hat), _lib.ptr(bits), B, _lib.stream_of(y.device)),
+                   "npd_sc_decode_lse")
+        return (hat, bits) if return_bits else hat
 
     # ------------------------------------------------------------------ Monte-Carlo extras
     def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False, out=None):

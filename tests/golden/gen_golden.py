@@ -8,6 +8,7 @@ Run in the build container only (``/root/reference`` does not exist on the GPU b
 Every fixture is data: inputs and the reference's outputs for them.  Reference functions called:
   PolarCode.__init__ / encode_plotkin / channel / sc_decode_new       polar.py:66-148, 201-207, 465-484
   PolarCode.scl_decode (use_CRC=False)                                polar.py:777-876
+  PolarCode.sc_decode / decode (exact-LSE SC, hard and soft)          polar.py:209-279
   PAC.__init__ / pac_encode / pac_sc_decode                           pac_code.py:97-224, 534-573
   rnn_all.get_code                                                    rnn_all.py:1015-1196
   RNN_Model / RNN_decoder.decode (test branch, y_input, onehot)       rnn_all.py:294-561
@@ -183,6 +184,36 @@ def gen_scl():
              msg_hat=np.concatenate(hats), info=np.asarray(code.info_positions, np.int64), L=np.int64(L))
 
 
+def gen_lse():
+    """PolarCode.sc_decode (exact-LSE SC, polar.py:209-279) with args.hard_decision True and False:
+    msg_hat and decoded_bits (decode(llrs, 0, 0, zeros) -- the call sc_decode makes, polar.py:221)."""
+    rng = np.random.default_rng(13)
+    for N, K, per in [(16, 8, 48), (32, 16, 48), (64, 32, 48), (128, 64, 24)]:
+        code = polar_code(N, K)
+        torch.manual_seed(4000 + N)
+        blocks = []
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (per, K)).float()
+            blocks.append((code.channel(code.encode_plotkin(msg), float(snr)), float(snr)))
+        for snr in (2.0, 4.0):  # zeros, |LLR| >> 200 (the NaN/inf patches), large and constant rows
+            blocks.append((torch.from_numpy(crafted_rows(N, rng)), snr))
+        out = {"y": np.concatenate([b.numpy() for b, _ in blocks]),
+               "snr": np.concatenate([np.full(b.shape[0], s) for b, s in blocks]),
+               "info": np.asarray(code.info_positions, np.int64)}
+        for hard in (True, False):
+            code.args = ns(hard_decision=hard)
+            hats, bits = [], []
+            for y, snr in blocks:
+                hats.append(code.sc_decode(y, snr).numpy())
+                llrs = (2 / utils_m.snr_db2sigma(snr) ** 2) * y
+                _, db = code.decode(llrs, 0, 0, torch.zeros(y.shape[0], N))
+                bits.append(db.numpy())
+            tag = "hard" if hard else "soft"
+            out[f"msg_hat_{tag}"] = np.concatenate(hats)
+            out[f"bits_{tag}"] = np.concatenate(bits)
+        save(f"lse_{N}_{K}.npz", **out)
+
+
 def gen_pac():
     rng = np.random.default_rng(6)
     for N, K, per in [(128, 64, 64), (64, 22, 96), (32, 16, 128)]:
@@ -301,6 +332,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "pac", "errors", "gru", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "lse", "pac", "errors", "gru", "conv"]
     for w in which:
         globals()["gen_" + w]()
