@@ -8,8 +8,10 @@
 //     default, "soft SC"), and the partial sums propagated up the tree are products of those values;
 //   * the output is sign(decoded_bits)[:, info] (polar.py:222), optionally decoded_bits itself.
 //
-// This decoder is transcendental-bound (4 exp/log per check node), not HBM-bound, so the design is the
-// simple one: one codeword per lane, the SC schedule walked iteratively (leaf i: one g step at depth
+// This decoder is transcendental-bound (4 exp/log per check node), not HBM-bound.  One codeword per
+// lane.  N <= 64 (lse_sc_reg_kernel, below): the tree is unrolled at compile time with every LLR level and
+// partial sum in VGPRs (156 VGPRs at N = 64, 3 waves/SIMD).  N >= 128 (lse_sc_kernel): the SC schedule is
+// walked iteratively (leaf i: one g step at depth
 // ctz(i)+1, f steps down to the leaf, partial-sum combines for the ctz(i+1) finished nodes), and the
 // per-lane LLR levels (N-1 floats) and partial sums (N floats) in LDS, lane-interleaved
 // (element e of lane l at dword e*64 + l: every access of a wave is conflict-free).  The root level is
@@ -19,6 +21,8 @@
 // every product opaque); exp/log/tanh are the device libm (<= 1 ulp, as is torch's CPU Sleef path),
 // so results agree with the reference to a few ulp and decisions agree except on near-zero LLRs
 // (tests/test_lse_gpu.py states the tolerance).
+#include <stdlib.h>
+
 #include "npd_common.hpp"
 
 namespace npd {
@@ -169,6 +173,101 @@ static int launch(const CodeParams& p, Args a, hipStream_t stream) {
     return launch_check("lse_sc_kernel launch");
 }
 
+// ------------------------------------------------------------------------------ register variant
+// N <= 64: the SC tree unrolled at compile time (template recursion over the nodes), every LLR level
+// and partial sum in a fixed VGPR (level d at lv[2^d, 2^(d+1)), the root at lv[N, 2N)): no LDS round
+// trips, and the independent check nodes of a level give the scheduler parallel exp/log chains.
+template <int N>
+struct RegState {
+    float lv[2 * N];
+    float beta[N];
+};
+
+template <int N, bool SOFT, int D, int S0>
+__device__ __forceinline__ void reg_node(RegState<N>& st, const CodeParams& p, float* ub, float* mh) {
+    if constexpr (D == 0) {
+        const bool frozen = (p.frozen[S0 >> 5] >> (S0 & 31)) & 1u;
+        float u = 1.0f;
+        if (!frozen) u = SOFT ? tanhf(st.lv[1] * 0.5f) : sgnf(st.lv[1]);
+        st.beta[S0] = u;
+        if (ub) ub[S0] = u;
+        if (mh && !frozen) mh[p.rank[S0]] = sgnf(u);
+    } else {
+        constexpr int h = 1 << (D - 1);
+#pragma unroll
+        for (int j = 0; j < h; ++j) st.lv[h + j] = lse_f(st.lv[2 * h + j], st.lv[3 * h + j]);
+        reg_node<N, SOFT, D - 1, S0>(st, p, ub, mh);
+#pragma unroll
+        for (int j = 0; j < h; ++j) st.lv[h + j] = lse_g(st.beta[S0 + j], st.lv[2 * h + j], st.lv[3 * h + j]);
+        reg_node<N, SOFT, D - 1, S0 + h>(st, p, ub, mh);
+        if constexpr ((1 << D) < N) {
+#pragma unroll
+            for (int j = 0; j < h; ++j) st.beta[S0 + j] = st.beta[S0 + j] * st.beta[S0 + h + j];
+        }
+    }
+}
+
+template <int N>
+constexpr int ilog2() {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    return n;
+}
+
+template <int N, bool SOFT>
+__global__ __launch_bounds__(64) void lse_sc_reg_kernel(const CodeParams p, const Args a) {
+    const int lane = threadIdx.x;
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t row = t * kWave + lane;
+        const bool valid = row < a.B;
+        const int64_t r = valid ? row : a.B - 1;
+        float* ub = (a.ubits && valid) ? a.ubits + row * N : nullptr;
+        float* mh = (a.msg && valid) ? a.msg + row * p.K : nullptr;
+        RegState<N> st;
+        const float4* yr = reinterpret_cast<const float4*>(a.y + r * N);
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q) {
+            const float4 v = yr[q];
+            st.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
+            st.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
+            st.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
+            st.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+        }
+        reg_node<N, SOFT, ilog2<N>(), 0>(st, p, ub, mh);
+    }
+}
+
+template <int N, bool SOFT>
+static int launch_reg(const CodeParams& p, Args a, hipStream_t stream) {
+    auto kern = lse_sc_reg_kernel<N, SOFT>;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, 0) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    a.ntiles = (a.B + kWave - 1) / kWave;
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), 0, stream, p, a);
+    return launch_check("lse_sc_reg_kernel launch");
+}
+
+template <bool SOFT>
+static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
+    // the register variant reads y rows as float4: 16-byte aligned rows only
+    const bool aligned = ((uintptr_t)a.y & 15u) == 0;
+    if (aligned) {
+        switch (p.N) {
+            case 4: return launch_reg<4, SOFT>(p, a, s);
+            case 8: return launch_reg<8, SOFT>(p, a, s);
+            case 16: return launch_reg<16, SOFT>(p, a, s);
+            case 32: return launch_reg<32, SOFT>(p, a, s);
+            case 64: return launch_reg<64, SOFT>(p, a, s);
+            default: break;
+        }
+    }
+    return launch<SOFT>(p, a, s);
+}
+
 }  // namespace lse
 }  // namespace npd
 
@@ -188,6 +287,10 @@ extern "C" int npd_sc_decode_lse(const npd_code* code, const float* y, float llr
     a.ubits = u_bits;
     a.B = B;
     a.scale = llr_scale;
-    return hard_decision ? lse::launch<false>(code->p, a, (hipStream_t)stream)
-                         : lse::launch<true>(code->p, a, (hipStream_t)stream);
+    if (getenv("NPD_LSE_LDS")) {  // force the LDS-resident variant (testing / A-B)
+        return hard_decision ? lse::launch<false>(code->p, a, (hipStream_t)stream)
+                             : lse::launch<true>(code->p, a, (hipStream_t)stream);
+    }
+    return hard_decision ? lse::dispatch<false>(code->p, a, (hipStream_t)stream)
+                         : lse::dispatch<true>(code->p, a, (hipStream_t)stream);
 }

@@ -113,3 +113,18 @@ def test_sc_decode_lse_full_size_properties(oracle):
         oh, _ = oracle.sc_decode_lse(ys.cpu().numpy(), 2.0, code.info_positions, hard)
         h = code.sc_decode(ys, 2.0, hard_decision=hard).cpu().numpy()
         check(h, None, oh, None, hard, hard)
+
+
+@pytest.mark.parametrize("N,K", [(8, 4), (32, 16), (64, 32)])
+def test_register_and_lds_variants_agree(monkeypatch, N, K):
+    """N <= 64 runs the register-resident kernel; NPD_LSE_LDS=1 forces the LDS-resident one (used for
+    N >= 128).  Same fp32 operation sequence -> identical bits in both decision modes."""
+    from neural_polar_decoder_amd import reference_polar_code
+    code = reference_polar_code(N, K)
+    _, _, y = code.mc_generate(3001, 1.0, seed=9, want_msg=False)
+    for hard in (True, False):
+        h1, b1 = code.sc_decode(y, 1.0, hard_decision=hard, return_bits=True)
+        monkeypatch.setenv("NPD_LSE_LDS", "1")
+        h2, b2 = code.sc_decode(y, 1.0, hard_decision=hard, return_bits=True)
+        monkeypatch.delenv("NPD_LSE_LDS")
+        assert torch.equal(h1, h2) and torch.equal(torch.nan_to_num(b1, nan=7.0), torch.nan_to_num(b2, nan=7.0))
