@@ -143,6 +143,24 @@ class SCLMonteCarlo(SCMonteCarlo):
         return MonteCarlo.count_sweep(self, cw_offset, n, counters)
 
 
+class LSEMonteCarlo(SCMonteCarlo):
+    """Exact-LSE SC decoding (PolarCode.sc_decode, polar.py:209-279; hard or soft decisions): fused
+    generate + npd_sc_decode_lse + device error counting."""
+
+    def __init__(self, code, snrs, total_cw, batch, seed=1234, hard_decision=False, rank=None, world=None,
+                 device=None):
+        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device)
+        self.hard_decision = bool(hard_decision)
+
+    def count_batch(self, si, snr, cw_offset, n, counters_row):
+        from .utils import count_errors
+        msg, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=True)
+        count_errors(msg, self.code.sc_decode(y, snr, hard_decision=self.hard_decision), counters_row)
+
+    def count_sweep(self, cw_offset, n, counters):
+        return MonteCarlo.count_sweep(self, cw_offset, n, counters)
+
+
 class GRUMonteCarlo(MonteCarlo):
     """CRISP GRU decoding (rnn_all.py:874-878): decoded[:, info] vs the message, counted on device."""
 
@@ -175,6 +193,8 @@ def _main(argv=None):
     ap.add_argument("--batch_size", type=int, default=1 << 20)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--list_size", type=int, default=None, help="also run SC-List with this list size (Polar)")
+    ap.add_argument("--lse", action="store_true", help="also run the exact-LSE sc_decode (Polar, polar.py:209)")
+    ap.add_argument("--hard_decision", action="store_true", help="exact-LSE SC with sign decisions (else tanh)")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
@@ -198,6 +218,11 @@ def _main(argv=None):
         if a.code != "polar":
             raise SystemExit("--list_size: SC-List is defined for Polar codes only (polar.py:793)")
         scl = SCLMonteCarlo(code, a.list_size, snrs, a.test_size, a.batch_size, a.seed).run()
+    lse = None
+    if a.lse:
+        if a.code != "polar":
+            raise SystemExit("--lse: the exact-LSE sc_decode is defined for Polar codes only (polar.py:209)")
+        lse = LSEMonteCarlo(code, snrs, a.test_size, a.batch_size, a.seed, hard_decision=a.hard_decision).run()
     if _dist() is None or _dist().get_rank() == 0:
         print("Test SNRs : ", snrs)
         print("BERs of SC decoding: {0}".format(res.ber))
@@ -207,6 +232,10 @@ def _main(argv=None):
             print("BERs of SCL decoding: {0}".format(scl.ber))
             print("BLERs of SCL decoding: {0}".format(scl.bler))
             rec["scl"] = dict(scl.as_dict(), list_size=a.list_size)
+        if lse is not None:
+            print("BERs of exact-LSE SC decoding: {0}".format(lse.ber))
+            print("BLERs of exact-LSE SC decoding: {0}".format(lse.bler))
+            rec["sc_lse"] = dict(lse.as_dict(), hard_decision=a.hard_decision)
         print(json.dumps(rec))
     return res
 

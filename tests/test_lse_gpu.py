@@ -128,3 +128,16 @@ def test_register_and_lds_variants_agree(monkeypatch, N, K):
         h2, b2 = code.sc_decode(y, 1.0, hard_decision=hard, return_bits=True)
         monkeypatch.delenv("NPD_LSE_LDS")
         assert torch.equal(h1, h2) and torch.equal(torch.nan_to_num(b1, nan=7.0), torch.nan_to_num(b2, nan=7.0))
+
+
+def test_lse_montecarlo_driver_and_cli(capsys):
+    """LSEMonteCarlo: shard invariance (3 simulated ranks == 1) and the CLI's --lse output."""
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import LSEMonteCarlo, _main
+    code = reference_polar_code(64, 32)
+    one = LSEMonteCarlo(code, [1.0, 2.0], 50_001, 20_000, seed=3, rank=0, world=1).run()
+    parts = [LSEMonteCarlo(code, [1.0, 2.0], 50_001, 20_000, seed=3, rank=r, world=3).run() for r in range(3)]
+    assert [sum(p.bit_errors[i] for p in parts) for i in range(2)] == one.bit_errors
+    assert 0.04 < one.ber[1] < 0.062
+    _main(["--test_size", "8192", "--batch_size", "4096", "--lse", "--snr_points", "2"])
+    assert "BERs of exact-LSE SC decoding" in capsys.readouterr().out
