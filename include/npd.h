@@ -118,6 +118,16 @@ int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_scale, floa
 int npd_sc_decode_lse(const npd_code* code, const float* y, float llr_scale, int hard_decision, float* msg_hat,
                       float* u_bits, int64_t B, void* stream);
 
+/*
+ * Soft-output SC, PolarCode.sc_decode_soft(noisy_code, snr, priors) (polar.py:281-358): LSE check
+ * nodes, leaf L^ = clamp(L + prior, -1000, 1000), right-child input LSE(L^_left, L_a) + L_b, nodes
+ * return [LSE(L^_u, L^_v), L^_v]; frozen positions get no special treatment (priors carry them).
+ * priors: HOST array of N floats or NULL (zeros).  Outputs as npd_sc_decode_lse.  N <= 64, y 16-byte
+ * aligned.
+ */
+int npd_sc_decode_soft(const npd_code* code, const float* y, float llr_scale, int hard_decision, const float* priors,
+                       float* msg_hat, float* u_bits, int64_t B, void* stream);
+
 /* ---------------------------------------------------------------------------------- SC-List decode */
 /*
  * Successive-cancellation list decoding, PolarCode.scl_decode(y, snr, L, use_CRC=False)

@@ -268,6 +268,96 @@ static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
     return launch<SOFT>(p, a, s);
 }
 
+// ------------------------------------------------------------------------------ soft SC (sc_decode_soft)
+// PolarCode.sc_decode_soft / decode_soft (polar.py:281-358): the same tree, but every node returns LLRs
+// instead of partial sums -- leaf: L^ = clamp(L + prior, -1000, 1000) (utils.py:259-263 with the 1e-10
+// margins vanishing in fp32), decided sign/tanh; right child input LSE(L^_left, L_a) + L_b; node return
+// [LSE(L^_u, L^_v), L^_v].  No frozen handling (priors carry it).  N <= 64, register-resident.
+struct SoftArgs {
+    const float* y;
+    float* msg;
+    float* ubits;
+    int64_t B;
+    int64_t ntiles;
+    float scale;
+    float prior[64];
+};
+
+__device__ __forceinline__ float clamp1000(float x) { return x < -1000.0f ? -1000.0f : (x > 1000.0f ? 1000.0f : x); }
+
+template <int N, bool SOFT, int D, int S0>
+__device__ __forceinline__ void soft_node(RegState<N>& st, const CodeParams& p, const SoftArgs& a, float* ub, float* mh) {
+    if constexpr (D == 0) {
+        const float L = clamp1000(st.lv[1] + a.prior[S0]);
+        const float u = SOFT ? tanhf(L * 0.5f) : sgnf(L);
+        st.beta[S0] = L;
+        if (ub) ub[S0] = u;
+        const bool frozen = (p.frozen[S0 >> 5] >> (S0 & 31)) & 1u;
+        if (mh && !frozen) mh[p.rank[S0]] = sgnf(u);
+    } else {
+        constexpr int h = 1 << (D - 1);
+#pragma unroll
+        for (int j = 0; j < h; ++j) st.lv[h + j] = lse_f(st.lv[2 * h + j], st.lv[3 * h + j]);
+        soft_node<N, SOFT, D - 1, S0>(st, p, a, ub, mh);
+#pragma unroll
+        for (int j = 0; j < h; ++j) st.lv[h + j] = lse_f(st.beta[S0 + j], st.lv[2 * h + j]) + st.lv[3 * h + j];
+        soft_node<N, SOFT, D - 1, S0 + h>(st, p, a, ub, mh);
+        if constexpr ((1 << D) < N) {  // the root's returned LLRs are never used
+#pragma unroll
+            for (int j = 0; j < h; ++j) st.beta[S0 + j] = lse_f(st.beta[S0 + j], st.beta[S0 + h + j]);
+        }
+    }
+}
+
+template <int N, bool SOFT>
+__global__ __launch_bounds__(64) void lse_soft_sc_kernel(const CodeParams p, const SoftArgs a) {
+    const int lane = threadIdx.x;
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t row = t * kWave + lane;
+        const bool valid = row < a.B;
+        const int64_t r = valid ? row : a.B - 1;
+        float* ub = (a.ubits && valid) ? a.ubits + row * N : nullptr;
+        float* mh = (a.msg && valid) ? a.msg + row * p.K : nullptr;
+        RegState<N> st;
+        const float4* yr = reinterpret_cast<const float4*>(a.y + r * N);
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q) {
+            const float4 v = yr[q];
+            st.lv[N + 4 * q + 0] = rmul(a.scale, v.x);
+            st.lv[N + 4 * q + 1] = rmul(a.scale, v.y);
+            st.lv[N + 4 * q + 2] = rmul(a.scale, v.z);
+            st.lv[N + 4 * q + 3] = rmul(a.scale, v.w);
+        }
+        soft_node<N, SOFT, ilog2<N>(), 0>(st, p, a, ub, mh);
+    }
+}
+
+template <int N, bool SOFT>
+static int launch_soft(const CodeParams& p, SoftArgs a, hipStream_t stream) {
+    auto kern = lse_soft_sc_kernel<N, SOFT>;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, 0) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    a.ntiles = (a.B + kWave - 1) / kWave;
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), 0, stream, p, a);
+    return launch_check("lse_soft_sc_kernel launch");
+}
+
+template <bool SOFT>
+static int dispatch_soft(const CodeParams& p, const SoftArgs& a, hipStream_t s) {
+    switch (p.N) {
+        case 4: return launch_soft<4, SOFT>(p, a, s);
+        case 8: return launch_soft<8, SOFT>(p, a, s);
+        case 16: return launch_soft<16, SOFT>(p, a, s);
+        case 32: return launch_soft<32, SOFT>(p, a, s);
+        case 64: return launch_soft<64, SOFT>(p, a, s);
+        default: return fail(NPD_EINVAL, "npd_sc_decode_soft: N <= 64");
+    }
+}
+
 }  // namespace lse
 }  // namespace npd
 
@@ -293,4 +383,24 @@ extern "C" int npd_sc_decode_lse(const npd_code* code, const float* y, float llr
     }
     return hard_decision ? lse::dispatch<false>(code->p, a, (hipStream_t)stream)
                          : lse::dispatch<true>(code->p, a, (hipStream_t)stream);
+}
+
+extern "C" int npd_sc_decode_soft(const npd_code* code, const float* y, float llr_scale, int hard_decision,
+                                  const float* priors, float* msg_hat, float* u_bits, int64_t B, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_decode_soft: code is NULL");
+    NPD_ARG(!code->p.pac, "npd_sc_decode_soft: Polar codes only (PolarCode.sc_decode_soft)");
+    NPD_ARG(code->p.N <= 64, "npd_sc_decode_soft: N <= 64");
+    NPD_ARG(B >= 0, "npd_sc_decode_soft: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_soft: y is NULL");
+    NPD_ARG(((uintptr_t)y & 15u) == 0, "npd_sc_decode_soft: y must be 16-byte aligned");
+    if (B == 0) return NPD_OK;
+    lse::SoftArgs a{};
+    a.y = y;
+    a.msg = msg_hat;
+    a.ubits = u_bits;
+    a.B = B;
+    a.scale = llr_scale;
+    for (int i = 0; i < 64; ++i) a.prior[i] = (priors && i < code->p.N) ? priors[i] : 0.0f;
+    return hard_decision ? lse::dispatch_soft<false>(code->p, a, (hipStream_t)stream)
+                         : lse::dispatch_soft<true>(code->p, a, (hipStream_t)stream);
 }

@@ -9,6 +9,7 @@ through libnpd (HIP kernels, ctypes C-ABI).  Tensors must live on the GPU.
   .channel(code, snr)                                                           polar.py:201-207
   .sc_decode_new(corrupted_codewords, snr, use_gt=None) -> (leaf_llrs, msg_hat) polar.py:465-484
   .sc_decode(noisy_code, snr) -> msg_hat   (exact-LSE SC, hard or soft)         polar.py:209-279
+  .sc_decode_soft(noisy_code, snr, priors=None) -> msg_hat  (soft-output SC)     polar.py:281-358
 
 MI355X extras (no reference equivalent, used by the Monte-Carlo driver and bench):
   .mc_generate(B, snr, seed, snr_index, cw_offset)   fused msg -> encode -> AWGN on device
@@ -216,6 +217,31 @@ class PolarCode:
         _lib.check(_lib.load().npd_sc_decode_lse(self.code.h, _lib.ptr(y), llr_scale(snr), 1 if hard_decision else 0,
                                                  _lib.ptr(hat), _lib.ptr(bits), B, _lib.stream_of(y.device)),
                    "npd_sc_decode_lse")
+        return (hat, bits) if return_bits else hat
+
+    def sc_decode_soft(self, noisy_code, snr, priors=None, hard_decision=None, return_bits=False):
+        """PolarCode.sc_decode_soft (polar.py:281-358): soft-output SC -- every node returns LLRs
+        (LSE(L^_u, L^_v), L^_v), leaves clamp(L + prior, +-1000); frozen positions are not special (the
+        priors carry them, as in the reference).  Returns sign(decoded_bits)[:, info] (B,K).  N <= 64."""
+        _lib.require_gpu(noisy_code, "noisy_code")
+        if hard_decision is None:
+            hard_decision = bool(getattr(self.args, "hard_decision", False)) if self.args is not None else False
+        y = _aligned(_lib.f32c(noisy_code))
+        if y.dim() != 2 or y.shape[1] != self.N:
+            raise ValueError(f"noisy_code must be (batch, {self.N}), got {tuple(y.shape)}")
+        pr = None
+        if priors is not None:
+            pr = np.ascontiguousarray(np.asarray(priors.cpu() if torch.is_tensor(priors) else priors,
+                                                 dtype=np.float32).reshape(-1))
+            if pr.size != self.N:
+                raise ValueError(f"priors must hold N = {self.N} values")
+        B = y.shape[0]
+        hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
+        bits = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_bits else None
+        _lib.check(_lib.load().npd_sc_decode_soft(self.code.h, _lib.ptr(y), llr_scale(snr), 1 if hard_decision else 0,
+                                                  None if pr is None else pr.ctypes.data_as(ctypes.c_void_p),
+                                                  _lib.ptr(hat), _lib.ptr(bits), B, _lib.stream_of(y.device)),
+                   "npd_sc_decode_soft")
         return (hat, bits) if return_bits else hat
 
     # ------------------------------------------------------------------ Monte-Carlo extras

@@ -13,6 +13,8 @@
  *                                                    (the GPU kernel patches per element; the tests
  *                                                    pin that the two agree)
  *   log_sum_avoid_zero_NaN         utils.py:348-397  (close_1/close_2 blend written as in the reference)
+ *   PolarCode.sc_decode_soft       polar.py:281-358  decode_soft: nodes return LLRs, leaf clamp(L + prior,
+ *                                                    +-1000) (Clamp, utils.py:259-263), no frozen rule
  *
  * Compiled with -ffp-contract=off.  exp/log/tanh are glibc's; torch's CPU path uses Sleef (<= 1 ulp), so
  * agreement with the reference is within a tolerance, pinned by tests/golden/lse_*.npz.
@@ -126,6 +128,65 @@ void oracle_sc_decode_lse(const float* y, int64_t B, int N, int K, const int32_t
         for (int i = 0; i < N; ++i) llr[i] = llr_scale * y[b * N + i];
         lse_ctx c = {n, frozen, hard, bits};
         lse_decode(&c, llr, 0, 0, ret);
+        if (bits_out) memcpy(bits_out + b * N, bits, sizeof(float) * (size_t)N);
+        if (msg_hat)
+            for (int k = 0; k < K; ++k) msg_hat[b * K + k] = sgn(bits[info[k]]);
+    }
+}
+
+/* ------------------------------------------------------------------ soft SC (polar.py:281-358) */
+static inline float clamp1000(float x) { return x < -1000.0f ? -1000.0f : (x > 1000.0f ? 1000.0f : x); }
+
+typedef struct {
+    int n;
+    const float* prior;
+    int hard;
+    float* bits;
+} soft_ctx;
+
+/* decode_soft(llrs, depth, bit_position, prior) (polar.py:305-358); ret = returned LLR vector (2*half) */
+static void soft_decode(soft_ctx* c, const float* llrs, int depth, int bitpos, float* ret) {
+    const int half = 1 << (c->n - depth - 1);
+    if (depth == c->n - 1) {
+        const int lp = 2 * bitpos, rp = 2 * bitpos + 1;
+        float Lu, Luv, Lv, top;
+        log_sum_avoid_zero_nan(&llrs[0], &llrs[1], &Lu, 1);
+        Lu = clamp1000(Lu + c->prior[lp] * 1.0f);
+        float u = c->hard ? sgn(Lu) : tanhf(Lu / 2.0f);
+        log_sum_avoid_zero_nan(&Lu, &llrs[0], &Luv, 1);
+        Lv = Luv + llrs[1];
+        Lv = clamp1000(Lv + c->prior[rp] * 1.0f);
+        float v = c->hard ? sgn(Lv) : tanhf(Lv / 2.0f);
+        c->bits[lp] = u;
+        c->bits[rp] = v;
+        log_sum_avoid_zero_nan(&Lu, &Lv, &top, 1);
+        ret[0] = top;
+        ret[1] = Lv;
+        return;
+    }
+    float Lu[LSE_MAX_N / 2], Lhu[LSE_MAX_N / 2], Luv[LSE_MAX_N / 2], Lv[LSE_MAX_N / 2], Lhv[LSE_MAX_N / 2];
+    log_sum_avoid_zero_nan(llrs, llrs + half, Lu, half);
+    soft_decode(c, Lu, depth + 1, 2 * bitpos, Lhu);
+    log_sum_avoid_zero_nan(Lhu, llrs, Luv, half);
+    for (int j = 0; j < half; ++j) Lv[j] = Luv[j] + llrs[half + j];
+    soft_decode(c, Lv, depth + 1, 2 * bitpos + 1, Lhv);
+    log_sum_avoid_zero_nan(Lhu, Lhv, ret, half);
+    for (int j = 0; j < half; ++j) ret[half + j] = Lhv[j];
+}
+
+/* PolarCode.sc_decode_soft(y, snr, priors): msg_hat = sign(decoded_bits)[:, info]; priors (N) or NULL */
+void oracle_sc_decode_soft(const float* y, int64_t B, int N, int K, const int32_t* info, const float* priors,
+                           float llr_scale, int hard, float* msg_hat, float* bits_out) {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    float zeros[LSE_MAX_N] = {0};
+    const float* pr = priors ? priors : zeros;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < B; ++b) {
+        float llr[LSE_MAX_N], bits[LSE_MAX_N], ret[LSE_MAX_N];
+        for (int i = 0; i < N; ++i) llr[i] = llr_scale * y[b * N + i];
+        soft_ctx c = {n, pr, hard, bits};
+        soft_decode(&c, llr, 0, 0, ret);
         if (bits_out) memcpy(bits_out + b * N, bits, sizeof(float) * (size_t)N);
         if (msg_hat)
             for (int k = 0; k < K; ++k) msg_hat[b * K + k] = sgn(bits[info[k]]);

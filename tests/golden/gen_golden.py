@@ -9,6 +9,7 @@ Every fixture is data: inputs and the reference's outputs for them.  Reference f
   PolarCode.__init__ / encode_plotkin / channel / sc_decode_new       polar.py:66-148, 201-207, 465-484
   PolarCode.scl_decode (use_CRC=False)                                polar.py:777-876
   PolarCode.sc_decode / decode (exact-LSE SC, hard and soft)          polar.py:209-279
+  PolarCode.sc_decode_soft / decode_soft (priors None and random)     polar.py:281-358
   PAC.__init__ / pac_encode / pac_sc_decode                           pac_code.py:97-224, 534-573
   rnn_all.get_code                                                    rnn_all.py:1015-1196
   RNN_Model / RNN_decoder.decode (test branch, y_input, onehot)       rnn_all.py:294-561
@@ -214,6 +215,41 @@ def gen_lse():
         save(f"lse_{N}_{K}.npz", **out)
 
 
+def gen_lse_soft():
+    """PolarCode.sc_decode_soft (polar.py:281-358), hard and soft decisions, priors None and a random
+    prior vector (large priors on frozen positions, as a caller would pass them)."""
+    rng = np.random.default_rng(17)
+    for N, K, per in [(16, 8, 48), (32, 16, 48), (64, 32, 48)]:
+        code = polar_code(N, K)
+        torch.manual_seed(5000 + N)
+        blocks = []
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (per, K)).float()
+            blocks.append((code.channel(code.encode_plotkin(msg), float(snr)), float(snr)))
+        for snr in (2.0, 4.0):
+            blocks.append((torch.from_numpy(crafted_rows(N, rng)), snr))
+        prior = np.zeros(N, np.float32)
+        prior[np.asarray(code.frozen_positions)] = 20.0
+        prior += rng.standard_normal(N).astype(np.float32)
+        out = {"y": np.concatenate([b.numpy() for b, _ in blocks]),
+               "snr": np.concatenate([np.full(b.shape[0], s) for b, s in blocks]),
+               "info": np.asarray(code.info_positions, np.int64), "prior": prior}
+        for hard in (True, False):
+            code.args = ns(hard_decision=hard)
+            for ptag, pr in (("p0", None), ("pr", torch.from_numpy(prior))):
+                hats, bits = [], []
+                for y, snr in blocks:
+                    hats.append(code.sc_decode_soft(y, snr, priors=pr).numpy())
+                    llrs = (2 / utils_m.snr_db2sigma(snr) ** 2) * y
+                    prv = torch.zeros(N) if pr is None else pr
+                    _, db = code.decode_soft(llrs, 0, 0, prv, torch.zeros(y.shape[0], N))
+                    bits.append(db.numpy())
+                tag = ("hard" if hard else "soft") + "_" + ptag
+                out[f"msg_hat_{tag}"] = np.concatenate(hats)
+                out[f"bits_{tag}"] = np.concatenate(bits)
+        save(f"lse_soft_{N}_{K}.npz", **out)
+
+
 def gen_pac():
     rng = np.random.default_rng(6)
     for N, K, per in [(128, 64, 64), (64, 22, 96), (32, 16, 128)]:
@@ -332,6 +368,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "lse", "pac", "errors", "gru", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "lse", "lse_soft", "pac", "errors", "gru", "conv"]
     for w in which:
         globals()["gen_" + w]()

@@ -72,6 +72,7 @@ def test_null_pointer_errors_are_reported_not_fatal():
     assert L.npd_awgn(None, None, 16, 6, 1.0, 0, 0, 0, None) == -1             # N % 4 != 0
     assert L.npd_count_errors(None, None, 4, 4, None, None) == -1
     assert L.npd_sc_decode_lse(None, None, 1.0, 1, None, None, 16, None) == -1
+    assert L.npd_sc_decode_soft(None, None, 1.0, 1, None, None, None, 16, None) == -1
 
 
 def test_product_path_refuses_host_tensors():

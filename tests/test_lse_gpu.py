@@ -141,3 +141,46 @@ def test_lse_montecarlo_driver_and_cli(capsys):
     assert 0.04 < one.ber[1] < 0.062
     _main(["--test_size", "8192", "--batch_size", "4096", "--lse", "--snr_points", "2"])
     assert "BERs of exact-LSE SC decoding" in capsys.readouterr().out
+
+
+
+@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32)])
+def test_sc_decode_soft_golden(N, K):
+    """PolarCode.sc_decode_soft (polar.py:281-358) vs the reference's vectors: with priors the bars of
+    check(); without priors (frozen bits decoded like information bits: leaf 0 is cancellation noise,
+    see test_oracle_golden) >= 99.5 % of bits and >= 98 % of codewords."""
+    d = golden(f"lse_soft_{N}_{K}.npz")
+    code = polar_for(N, d["info"])
+    for hard in (True, False):
+        for ptag in ("p0", "pr"):
+            tag = ("hard" if hard else "soft") + "_" + ptag
+            hat = np.empty_like(d[f"msg_hat_{tag}"])
+            bits = np.empty_like(d[f"bits_{tag}"])
+            for s in np.unique(d["snr"]):
+                m = d["snr"] == s
+                h, b = code.sc_decode_soft(t(d["y"][m]), float(s), priors=None if ptag == "p0" else d["prior"],
+                                           hard_decision=hard, return_bits=True)
+                hat[m], bits[m] = h.cpu().numpy(), b.cpu().numpy()
+            if ptag == "pr":
+                check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag))
+            else:
+                ag = hat == d[f"msg_hat_{tag}"]
+                assert ag.mean() >= 0.995 and ag.all(axis=1).mean() >= 0.98, (N, tag)
+
+
+def test_sc_decode_soft_vs_oracle_random(oracle):
+    """Random words, ragged batches, priors from the frozen set (+20) plus noise, N = 8..64."""
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    for N, K in [(8, 4), (32, 16), (64, 32), (64, 22)]:
+        info = polar_info_positions(N, K)
+        code = polar_for(N, info)
+        rng = np.random.default_rng(N + 3 * K)
+        prior = np.zeros(N, np.float32)
+        prior[np.setdiff1d(np.arange(N), info)] = 20.0
+        prior += rng.standard_normal(N).astype(np.float32)
+        for B in (1, 65, 1000):
+            y = (rng.standard_normal((B, N)) * 0.8 + (1 - 2 * (rng.random((B, N)) < 0.5))).astype(np.float32)
+            for hard in (True, False):
+                h, b = code.sc_decode_soft(t(y), 2.5, priors=prior, hard_decision=hard, return_bits=True)
+                oh, ob = oracle.sc_decode_soft(y, 2.5, info, hard, prior)
+                check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard))

@@ -178,3 +178,30 @@ def test_sc_decode_lse_golden(oracle, N, K):
         else:
             assert (hat == g).mean() >= 0.999 and (hat == g).all(axis=1).mean() >= 0.99, (N, tag)
             np.testing.assert_allclose(bits, gb, rtol=0, atol=1e-4, equal_nan=True)
+
+
+@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32)])
+def test_sc_decode_soft_golden(oracle, N, K):
+    """PolarCode.sc_decode_soft (polar.py:281-358) with the fixture's priors ('pr': hard decisions
+    bit-exact, soft decoded_bits within 1e-4) and without ('p0': frozen bits are decoded like information
+    bits, so leaf 0's LLR is the cancellation-dominated boxplus of all N LLRs and its sign is rounding
+    noise of the formula -- >= 99.5 % of bits and >= 98 % of codewords identical)."""
+    d = golden(f"lse_soft_{N}_{K}.npz")
+    for hard in (True, False):
+        for ptag in ("p0", "pr"):
+            tag = ("hard" if hard else "soft") + "_" + ptag
+            hat = np.empty_like(d[f"msg_hat_{tag}"])
+            bits = np.empty_like(d[f"bits_{tag}"])
+            for s in np.unique(d["snr"]):
+                m = d["snr"] == s
+                hat[m], bits[m] = oracle.sc_decode_soft(d["y"][m], float(s), d["info"], hard,
+                                                        None if ptag == "p0" else d["prior"])
+            g, gb = d[f"msg_hat_{tag}"], d[f"bits_{tag}"]
+            if ptag == "pr":
+                assert (hat == g).all(), tag
+                if hard:
+                    assert np.array_equal(bits, gb), tag
+                else:
+                    np.testing.assert_allclose(bits, gb, rtol=0, atol=1e-4, equal_nan=True)
+            else:
+                assert (hat == g).mean() >= 0.995 and (hat == g).all(axis=1).mean() >= 0.98, tag
