@@ -1,4 +1,5 @@
-// npd_lse.hip -- exact log-sum-exp successive-cancellation decoding for gfx950.
+// npd_lse.hip -- exact log-sum-exp successive-cancellation decoding for gfx950
+// (PolarCode.sc_decode and, below, the soft-output PolarCode.sc_decode_soft).
 //
 // Replaces PolarCode.sc_decode / decode (polar.py:209-279): the same SC tree as sc_decode_new, but
 //   * the check-node update is the exact boxplus of utils.py:348-397 (log_sum_avoid_zero_NaN), not
