@@ -10,9 +10,9 @@
 //   * the output is sign(decoded_bits)[:, info] (polar.py:222), optionally decoded_bits itself.
 //
 // This decoder is transcendental-bound (4 exp/log per check node), not HBM-bound.  One codeword per
-// lane.  N <= 64 (lse_sc_reg_kernel, below): the tree is unrolled at compile time with every LLR level and
-// partial sum in VGPRs (156 VGPRs at N = 64, 3 waves/SIMD).  N >= 128 (lse_sc_kernel): the SC schedule is
-// walked iteratively (leaf i: one g step at depth
+// lane.  N <= 128 (lse_sc_reg_kernel, below): the tree is unrolled at compile time with every LLR level
+// and partial sum in registers (156 VGPRs at N = 64, 3 waves/SIMD; 256 + AGPRs at N = 128, 1 wave/SIMD,
+// no scratch).  N = 256 (lse_sc_kernel): the SC schedule is walked iteratively (leaf i: one g step at depth
 // ctz(i)+1, f steps down to the leaf, partial-sum combines for the ctz(i+1) finished nodes), and the
 // per-lane LLR levels (N-1 floats) and partial sums (N floats) in LDS, lane-interleaved
 // (element e of lane l at dword e*64 + l: every access of a wave is conflict-free).  The root level is
@@ -175,7 +175,7 @@ static int launch(const CodeParams& p, Args a, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------------------ register variant
-// N <= 64: the SC tree unrolled at compile time (template recursion over the nodes), every LLR level
+// N <= 128: the SC tree unrolled at compile time (template recursion over the nodes), every LLR level
 // and partial sum in a fixed VGPR (level d at lv[2^d, 2^(d+1)), the root at lv[N, 2N)): no LDS round
 // trips, and the independent check nodes of a level give the scheduler parallel exp/log chains.
 template <int N>
@@ -263,6 +263,7 @@ static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
             case 16: return launch_reg<16, SOFT>(p, a, s);
             case 32: return launch_reg<32, SOFT>(p, a, s);
             case 64: return launch_reg<64, SOFT>(p, a, s);
+            case 128: return launch_reg<128, SOFT>(p, a, s);
             default: break;
         }
     }

@@ -115,10 +115,10 @@ def test_sc_decode_lse_full_size_properties(oracle):
         check(h, None, oh, None, hard, hard)
 
 
-@pytest.mark.parametrize("N,K", [(8, 4), (32, 16), (64, 32)])
+@pytest.mark.parametrize("N,K", [(8, 4), (32, 16), (64, 32), (128, 64)])
 def test_register_and_lds_variants_agree(monkeypatch, N, K):
-    """N <= 64 runs the register-resident kernel; NPD_LSE_LDS=1 forces the LDS-resident one (used for
-    N >= 128).  Same fp32 operation sequence -> identical bits in both decision modes."""
+    """N <= 128 runs the register-resident kernel; NPD_LSE_LDS=1 forces the LDS-resident one (used for
+    N = 256).  Same fp32 operation sequence -> identical bits in both decision modes."""
     from neural_polar_decoder_amd import reference_polar_code
     code = reference_polar_code(N, K)
     _, _, y = code.mc_generate(3001, 1.0, seed=9, want_msg=False)

@@ -5,7 +5,7 @@ import torch
 sys.path.insert(0, ".")
 from neural_polar_decoder_amd import reference_polar_code
 from oracle import oracle as O
-for N, K, B in [(64, 32, 1 << 18), (256, 128, 1 << 16)]:
+for N, K, B in [(64, 32, 1 << 18), (128, 64, 1 << 17), (256, 128, 1 << 16)]:
     code = reference_polar_code(N, K)
     _, _, y = code.mc_generate(B, 2.0, 1234, 0, 0, want_msg=False)
     for hard in (False, True):
