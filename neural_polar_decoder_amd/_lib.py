@@ -2,6 +2,8 @@
 
 The product path has exactly one implementation: the HIP kernels in libnpd.so.  If the library is
 missing or no GPU is visible, every compute call raises :class:`NpdError` -- there is no CPU fallback.
+Host tensors given to the reference-surface methods are staged to the GPU (:func:`stage`) and the
+results copied back (:func:`home`); the compute stays on the GPU.
 """
 from __future__ import annotations
 
@@ -83,11 +85,39 @@ def check(rc: int, what: str = ""):
 
 
 def require_gpu(t: torch.Tensor, name: str):
-    """The product path runs only on the GPU: fail loudly for host tensors."""
+    """Device-only entry points (the Monte-Carlo extras): fail loudly for host tensors."""
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
     if not t.is_cuda:
         raise NpdError(f"{name} must be a device (HIP) tensor: libnpd has no CPU path")
+
+
+def compute_device() -> torch.device:
+    """The GPU that runs a call whose inputs live on the host: torch's current HIP device."""
+    if not torch.cuda.is_available():
+        raise NpdError("no GPU visible: libnpd computes only on the MI355X (there is no CPU path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stage(t, name: str, device: torch.device | None = None) -> torch.Tensor:
+    """Input of a reference-surface method as a device tensor.
+
+    The reference's eval loops hand some methods host tensors (``polar.scl_decode(noisy_code.cpu(), ...)``
+    run_models.py:329, rnn_all.py:858; ``errors_ber(msg_bits.cpu(), ...)`` run_models.py:330-336).
+    Those are copied to ``device`` (default: the current HIP device) and computed on the GPU; the caller
+    returns results with :func:`home`.  Device tensors pass through untouched (no copy, no sync)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.is_cuda:
+        return t if device is None or t.device == device else t.to(device)
+    return t.to(device if device is not None else compute_device())
+
+
+def home(t: torch.Tensor | None, like: torch.Tensor):
+    """Return a result on the device of the caller's input ``like`` (host results of host inputs)."""
+    if t is None or t.device == like.device:
+        return t
+    return t.to(like.device)
 
 
 def ptr(t):

@@ -83,10 +83,9 @@ class convNet(nn.Module):
             pass
 
     def logits(self, noisy_enc: torch.Tensor, want_decisions=True):
-        _lib.require_gpu(noisy_enc, "noisy_enc")
         if self.training:
             raise _lib.NpdError("the fused convNet path is inference-only (eval mode)")
-        y = _lib.f32c(noisy_enc)
+        y = _lib.f32c(_lib.stage(noisy_enc, "noisy_enc"))
         B = y.shape[0]
         if y.shape[1] != self.output_len:
             raise ValueError("input length must equal config.N (= max_len)")
@@ -98,7 +97,7 @@ class convNet(nn.Module):
         dec = torch.empty_like(lg) if want_decisions else None
         _lib.check(L.npd_conv_forward(h, _lib.ptr(y), _lib.ptr(lg), _lib.ptr(dec), _lib.ptr(ws), B,
                                       _lib.stream_of(y.device)), "npd_conv_forward")
-        return lg, dec
+        return _lib.home(lg, noisy_enc), _lib.home(dec, noisy_enc)
 
     def forward(self, noisy_enc, mask, trg_seq, device):
         """models.py:742-767: returns (output, decoded_msg_bits, out_mask, logits, None); the

@@ -7,7 +7,8 @@
   .channel(code, snr)                                                 pac_code.py:226-231
   .pac_sc_decode(y, snr, use_gt_codeword=None) -> (llr, v_hat[:,B], u_hat)   pac_code.py:534-573
   .extract(v_hat, B=None)                                             pac_code.py:528-531
-All compute runs in libnpd's HIP kernels; tensors must live on the GPU.
+All compute runs in libnpd's HIP kernels; host inputs are staged to the current GPU and results come
+back on the input's device.
 """
 from __future__ import annotations
 
@@ -78,53 +79,54 @@ class PAC:
         return u
 
     def pac_encode(self, msg_bits, scheme=None, custom_info_positions=None):
-        _lib.require_gpu(msg_bits, "msg_bits")
         B = self._set_for(scheme, custom_info_positions)
         self.B = B
         h = self._code_for(B)
-        msg = _lib.f32c(msg_bits)
+        msg = _lib.f32c(_lib.stage(msg_bits, "msg_bits"))
         x = torch.empty(msg.shape[0], self.N, dtype=torch.float32, device=msg.device)
         _lib.check(_lib.load().npd_encode(h.h, _lib.ptr(msg), _lib.ptr(x), msg.shape[0], _lib.stream_of(msg.device)),
                    "npd_encode")
-        return x
+        return _lib.home(x, msg_bits)
 
     encode = pac_encode
 
     def polar_encode(self, msg_bits):
         """Rate-1 Plotkin transform of u (B,N)."""
-        _lib.require_gpu(msg_bits, "msg_bits")
         if self._rate1 is None:
             self._rate1 = _CodeHandle(self.N, np.arange(self.N), 0, self.infty)
-        u = _lib.f32c(msg_bits)
+        u = _lib.f32c(_lib.stage(msg_bits, "msg_bits"))
         x = torch.empty_like(u)
         _lib.check(_lib.load().npd_encode(self._rate1.h, _lib.ptr(u), _lib.ptr(x), u.shape[0], _lib.stream_of(u.device)),
                    "npd_encode")
-        return x
+        return _lib.home(x, msg_bits)
 
     # ------------------------------------------------------------------ channel
-    def channel(self, code, snr, snr_index: int = 0):
-        _lib.require_gpu(code, "code")
-        x = _lib.f32c(code)
+    def channel(self, code, snr, noise_type="awgn", vv=None, radar_power=None, radar_prob=None, *, snr_index: int = 0):
+        """y = x + sigma * N(0,1); the extra arguments accept rnn.py:754's 6-argument call (AWGN only)."""
+        if noise_type not in (None, "awgn"):
+            raise NotImplementedError(f"noise_type {noise_type!r}: the reference defines only the AWGN channel "
+                                      "(pac_code.py:226-231)")
+        x = _lib.f32c(_lib.stage(code, "code"))
         Bn, N = x.shape
         y = torch.empty_like(x)
         off = self._rng.take(Bn)
         _lib.check(_lib.load().npd_awgn(_lib.ptr(x), _lib.ptr(y), Bn, N, sigma_f32(snr), self._rng.seed, int(snr_index),
                                         off, _lib.stream_of(x.device)), "npd_awgn")
-        return y
+        return _lib.home(y, code)
 
     # ------------------------------------------------------------------ SC (pac_code.py:534-573)
     def pac_sc_decode(self, corrupted_codewords, snr, use_gt_codeword=None):
-        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
-        y = _lib.f32c(corrupted_codewords)
+        y = _lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords"))
         Bn = y.shape[0]
         h = self._code_for(self.B)
         llr = torch.empty(Bn, self.N, dtype=torch.float32, device=y.device)
         vh = torch.empty(Bn, h.K, dtype=torch.float32, device=y.device)
         uh = torch.empty(Bn, self.N, dtype=torch.float32, device=y.device)
-        gt = None if use_gt_codeword is None else _lib.f32c(use_gt_codeword.to(y.device))
+        gt = None if use_gt_codeword is None else _lib.f32c(_lib.stage(use_gt_codeword, "use_gt_codeword", y.device))
         _lib.check(_lib.load().npd_sc_decode(h.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(llr), _lib.ptr(vh), _lib.ptr(uh),
                                              _lib.ptr(gt), Bn, _lib.stream_of(y.device)), "npd_sc_decode")
-        return llr, vh, uh
+        c = corrupted_codewords
+        return _lib.home(llr, c), _lib.home(vh, c), _lib.home(uh, c)
 
     def extract(self, v_hat, B=None):
         if B is None:

@@ -1,12 +1,14 @@
 """PolarCode -- drop-in for the reference's ``polar.PolarCode`` hot-path surface (polar.py:64-484).
 
 Same constructor and method signatures as the reference; every compute method runs on the MI355X
-through libnpd (HIP kernels, ctypes C-ABI).  Tensors must live on the GPU.
+through libnpd (HIP kernels, ctypes C-ABI).  Host tensors (the eval loops pass ``noisy_code.cpu()``
+to ``scl_decode``, run_models.py:329) are staged to the current GPU and results come back on the
+input's device.
 
   PolarCode(n, K, args=None, F=None, rs=None, use_cuda=True, infty=1000.)      polar.py:66-117
   .encode_plotkin(message, scaling=None, custom_info_positions=None)            polar.py:128-148
   .encode  (alias of encode_plotkin, as rnn_all.get_code sets it, rnn_all.py:1187)
-  .channel(code, snr)                                                           polar.py:201-207
+  .channel(code, snr[, noise_type, vv, radar_power, radar_prob])                polar.py:201-207
   .sc_decode_new(corrupted_codewords, snr, use_gt=None) -> (leaf_llrs, msg_hat) polar.py:465-484
   .sc_decode(noisy_code, snr) -> msg_hat   (exact-LSE SC, hard or soft)         polar.py:209-279
   .sc_decode_soft(noisy_code, snr, priors=None) -> msg_hat  (soft-output SC)     polar.py:281-358
@@ -118,52 +120,54 @@ class PolarCode:
 
     # ------------------------------------------------------------------ encoder (polar.py:128-148)
     def encode_plotkin(self, message, scaling=None, custom_info_positions=None):
-        _lib.require_gpu(message, "message")
         h = self._code_for(custom_info_positions)
-        msg = _lib.f32c(message)
+        msg = _lib.f32c(_lib.stage(message, "message"))
         if msg.dim() != 2 or msg.shape[1] != h.K:
             raise ValueError(f"message must be (batch, {h.K}), got {tuple(msg.shape)}")
         x = torch.empty(msg.shape[0], self.N, dtype=torch.float32, device=msg.device)
         _lib.check(_lib.load().npd_encode(h.h, _lib.ptr(msg), _lib.ptr(x), msg.shape[0], _lib.stream_of(msg.device)),
                    "npd_encode")
         if scaling is not None:
-            x = (scaling * np.sqrt(self.N) * x) / torch.norm(scaling)
-        return x
+            x = (scaling.to(x.device) * np.sqrt(self.N) * x) / torch.norm(scaling)
+        return _lib.home(x, message)
 
     encode = encode_plotkin
 
     # ------------------------------------------------------------------ channel (polar.py:201-207)
-    def channel(self, code, snr, snr_index: int = 0):
-        _lib.require_gpu(code, "code")
-        x = _lib.f32c(code)
+    def channel(self, code, snr, noise_type="awgn", vv=None, radar_power=None, radar_prob=None, *, snr_index: int = 0):
+        """y = x + sigma * N(0,1).  The extra arguments are the 6-argument call of rnn_all.py:847 /
+        rnn.py:864 (which the reference's own 2-argument channel rejects); only 'awgn' is defined in
+        the reference's code, so other noise types raise."""
+        if noise_type not in (None, "awgn"):
+            raise NotImplementedError(f"noise_type {noise_type!r}: the reference defines only the AWGN channel "
+                                      "(polar.py:201-207)")
+        x = _lib.f32c(_lib.stage(code, "code"))
         B, N = x.shape
         y = torch.empty_like(x)
         off = self._rng.take(B)
         _lib.check(_lib.load().npd_awgn(_lib.ptr(x), _lib.ptr(y), B, N, sigma_f32(snr), self._rng.seed, int(snr_index),
                                         off, _lib.stream_of(x.device)), "npd_awgn")
-        return y
+        return _lib.home(y, code)
 
     # ------------------------------------------------------------------ SC (polar.py:465-484)
     def sc_decode_new(self, corrupted_codewords, snr, use_gt=None):
         """Min-sum SC; returns (leaf LLRs incl. the frozen prior (B,N), msg_hat (B,K)) bit-exactly."""
-        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
-        y = _lib.f32c(corrupted_codewords)
+        y = _lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords"))
         B = y.shape[0]
         leaf = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
         hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
-        gt = None if use_gt is None else _lib.f32c(use_gt.to(y.device))
+        gt = None if use_gt is None else _lib.f32c(_lib.stage(use_gt, "use_gt", y.device))
         _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(leaf), _lib.ptr(hat), None,
                                              _lib.ptr(gt), B, _lib.stream_of(y.device)), "npd_sc_decode")
-        return leaf, hat
+        return _lib.home(leaf, corrupted_codewords), _lib.home(hat, corrupted_codewords)
 
     def sc_decode_msg(self, corrupted_codewords, snr):
         """msg_hat only (no leaf LLR traffic): the form the BER/BLER loops consume."""
-        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
-        y = _lib.f32c(corrupted_codewords)
+        y = _lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords"))
         hat = torch.empty(y.shape[0], self.K, dtype=torch.float32, device=y.device)
         _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), None, _lib.ptr(hat), None, None,
                                              y.shape[0], _lib.stream_of(y.device)), "npd_sc_decode")
-        return hat
+        return _lib.home(hat, corrupted_codewords)
 
     # ------------------------------------------------------------------ SC-List (polar.py:793-876)
     def scl_decode(self, corrupted_codewords, snr, L=1, use_CRC=False, want_llrs=True):
@@ -174,8 +178,7 @@ class PolarCode:
         if use_CRC:
             raise NotImplementedError("scl_decode(use_CRC=True) depends on module globals of the reference "
                                       "(polar.py:741-763: `polar.CRC_len`); only the use_CRC=False path is built")
-        _lib.require_gpu(corrupted_codewords, "corrupted_codewords")
-        y = _aligned(_lib.f32c(corrupted_codewords))
+        y = _aligned(_lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords")))
         B = y.shape[0]
         hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
         uh = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if want_llrs else None
@@ -183,11 +186,11 @@ class PolarCode:
         _lib.check(_lib.load().npd_scl_decode(self.code.h, _lib.ptr(y), llr_scale(snr), int(L), _lib.ptr(hat),
                                               _lib.ptr(uh), B, st), "npd_scl_decode")
         if not want_llrs:
-            return None, hat
+            return None, _lib.home(hat, corrupted_codewords)
         leaf = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
         _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(leaf), None, None,
                                              _lib.ptr(uh), B, st), "npd_sc_decode (genie leaf LLRs)")
-        return leaf, hat
+        return _lib.home(leaf, corrupted_codewords), _lib.home(hat, corrupted_codewords)
 
     def scl_decode_mc(self, y, snr, L, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
@@ -205,10 +208,9 @@ class PolarCode:
         Decisions follow ``self.args.hard_decision`` as in the reference (sign(L) if set, else the soft
         tanh(L/2) -- argparse's default); ``hard_decision=`` overrides it.  ``return_bits=True`` also
         returns decoded_bits (B,N).  Not the min-sum ``sc_decode_new`` the eval loops call."""
-        _lib.require_gpu(noisy_code, "noisy_code")
         if hard_decision is None:
             hard_decision = bool(getattr(self.args, "hard_decision", False)) if self.args is not None else False
-        y = _lib.f32c(noisy_code)
+        y = _lib.f32c(_lib.stage(noisy_code, "noisy_code"))
         if y.dim() != 2 or y.shape[1] != self.N:
             raise ValueError(f"noisy_code must be (batch, {self.N}), got {tuple(y.shape)}")
         B = y.shape[0]
@@ -217,16 +219,16 @@ class PolarCode:
         _lib.check(_lib.load().npd_sc_decode_lse(self.code.h, _lib.ptr(y), llr_scale(snr), 1 if hard_decision else 0,
                                                  _lib.ptr(hat), _lib.ptr(bits), B, _lib.stream_of(y.device)),
                    "npd_sc_decode_lse")
-        return (hat, bits) if return_bits else hat
+        hat = _lib.home(hat, noisy_code)
+        return (hat, _lib.home(bits, noisy_code)) if return_bits else hat
 
     def sc_decode_soft(self, noisy_code, snr, priors=None, hard_decision=None, return_bits=False):
         """PolarCode.sc_decode_soft (polar.py:281-358): soft-output SC -- every node returns LLRs
         (LSE(L^_u, L^_v), L^_v), leaves clamp(L + prior, +-1000); frozen positions are not special (the
         priors carry them, as in the reference).  Returns sign(decoded_bits)[:, info] (B,K).  N <= 64."""
-        _lib.require_gpu(noisy_code, "noisy_code")
         if hard_decision is None:
             hard_decision = bool(getattr(self.args, "hard_decision", False)) if self.args is not None else False
-        y = _aligned(_lib.f32c(noisy_code))
+        y = _aligned(_lib.f32c(_lib.stage(noisy_code, "noisy_code")))
         if y.dim() != 2 or y.shape[1] != self.N:
             raise ValueError(f"noisy_code must be (batch, {self.N}), got {tuple(y.shape)}")
         pr = None
@@ -242,7 +244,8 @@ class PolarCode:
                                                   None if pr is None else pr.ctypes.data_as(ctypes.c_void_p),
                                                   _lib.ptr(hat), _lib.ptr(bits), B, _lib.stream_of(y.device)),
                    "npd_sc_decode_soft")
-        return (hat, bits) if return_bits else hat
+        hat = _lib.home(hat, noisy_code)
+        return (hat, _lib.home(bits, noisy_code)) if return_bits else hat
 
     # ------------------------------------------------------------------ Monte-Carlo extras
     def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False, out=None):

@@ -137,8 +137,8 @@ class RNN_decoder:
             raise _lib.NpdError("network configuration not supported by the fused GRU decoder")
         if net.input_size != self.N + 1 + int(self.onehot):
             raise ValueError("net.input_size must be N + 1 + onehot")
-        _lib.require_gpu(y, "y")
-        y = _lib.f32c(y)
+        y_in = y
+        y = _lib.f32c(_lib.stage(y, "y"))
         B = y.shape[0]
         if loss_inds is None:
             loss_inds = self.info_inds
@@ -147,11 +147,12 @@ class RNN_decoder:
         h = self._handle(net, y.device)
         dec = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
         logits = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_logits else None
-        g = None if gt is None else _lib.f32c(gt.to(y.device))
+        g = None if gt is None else _lib.f32c(_lib.stage(gt, "gt", y.device))
         _lib.check(_lib.load().npd_gru_decode(h.h, _lib.ptr(y), is_info.ctypes.data_as(ctypes.c_void_p),
                                               1 if self.reverse_order else 0, _lib.ptr(g), _lib.ptr(dec),
                                               _lib.ptr(logits), B, _lib.stream_of(y.device)), "npd_gru_decode")
-        return (dec, logits) if return_logits else dec
+        dec = _lib.home(dec, y_in)
+        return (dec, _lib.home(logits, y_in)) if return_logits else dec
 
 
 def get_onehot(actions):

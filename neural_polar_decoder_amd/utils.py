@@ -1,8 +1,9 @@
 """Numerics helpers and error counters with the reference's semantics (utils.py:5-51).
 
-``errors_ber`` / ``errors_bler`` keep the reference's signatures and return values but count on
-the GPU (npd_count_errors) into device uint64 counters: no per-batch host round trip
-(the reference copies to numpy in errors_bler, utils.py:41-45).
+``errors_ber`` / ``errors_bler`` keep the reference's signatures and return types (a (1,) float32
+tensor on the input's device / a ``numpy.float64``) but count on the GPU (npd_count_errors) into
+device uint64 counters.  Host inputs (the eval loops pass ``msg_bits.cpu()``, run_models.py:330-336)
+are staged to the GPU first.
 """
 from __future__ import annotations
 
@@ -28,40 +29,69 @@ def sigma_f32(snr) -> float:
 
 
 def count_errors(y_true: torch.Tensor, y_pred: torch.Tensor, counters: torch.Tensor | None = None) -> torch.Tensor:
-    """Device counters [bit errors, block errors] (uint64 stored in an int64 tensor), accumulated."""
-    _lib.require_gpu(y_true, "y_true")
-    _lib.require_gpu(y_pred, "y_pred")
-    t = _lib.f32c(y_true.reshape(y_true.shape[0], -1))
-    p = _lib.f32c(y_pred.reshape(y_pred.shape[0], -1))
+    """Device counters [bit errors, block errors] (uint64 stored in an int64 tensor), accumulated.
+
+    Host inputs are staged to the GPU of ``counters`` (or the current HIP device)."""
+    dev = counters.device if counters is not None and counters.is_cuda else None
+    t = _lib.stage(y_true, "y_true", dev)
+    p = _lib.stage(y_pred, "y_pred", t.device)
+    t = _lib.f32c(t.reshape(t.shape[0], -1))
+    p = _lib.f32c(p.reshape(p.shape[0], -1))
     if t.shape != p.shape:
         raise ValueError(f"shape mismatch {tuple(t.shape)} vs {tuple(p.shape)}")
     if counters is None:
         counters = torch.zeros(2, dtype=torch.int64, device=t.device)
+    _lib.require_gpu(counters, "counters")
     L = _lib.load()
     _lib.check(L.npd_count_errors(_lib.ptr(t), _lib.ptr(p), t.shape[0], t.shape[1], _lib.ptr(counters),
                                   _lib.stream_of(t.device)), "npd_count_errors")
     return counters
 
 
+def _masked_errors(y_true, y_pred, mask):
+    """(mask * (round(true) != round(pred))) as float on the GPU, per element (utils.py:20-23)."""
+    t = _lib.stage(y_true, "y_true")
+    p = _lib.stage(y_pred, "y_pred", t.device)
+    t = t.reshape(t.shape[0], -1, 1)
+    p = p.reshape(p.shape[0], -1, 1)
+    m = _lib.stage(mask, "mask", t.device).reshape(mask.shape[0], -1, 1)
+    return (m * torch.ne(torch.round(t), torch.round(p))).float(), m
+
+
 def errors_ber(y_true, y_pred, mask=None):
-    """Bit error rate (utils.py:17-25): mean of round(true) != round(pred). Returns a 0-dim tensor."""
+    """Bit error rate (utils.py:17-25): mean of round(true) != round(pred) over the mask.
+
+    Returns what the reference returns -- a float32 tensor of shape (1,) on ``y_true``'s device
+    (``sum(sum(x)) / torch.sum(mask)``) -- so the eval loops' ``.item()`` works unchanged.  The count is
+    exact (device uint64) and divided in fp32 like the reference's float sums.  A mask with any entry
+    other than 1 takes the reference's formula, evaluated on the GPU."""
     if mask is not None and not bool(torch.all(mask == 1)):
-        # masked form is only used with all-ones masks in the eval loops (run_models.py:323-341)
-        y_true = y_true.reshape(y_true.shape[0], -1)
-        y_pred = y_pred.reshape(y_pred.shape[0], -1)
-        m = mask.reshape(mask.shape[0], -1).to(y_true.dtype)
-        return (m * torch.ne(torch.round(y_true), torch.round(y_pred)).float()).sum() / m.sum()
+        e, m = _masked_errors(y_true, y_pred, mask)
+        res = (e.sum() / torch.sum(m)).reshape(1).float()
+        return _lib.home(res, y_true)
     c = count_errors(y_true, y_pred)
     n = y_true.numel()
-    return c[0].double() / n
+    res = c[0:1].float() / torch.tensor(float(n), dtype=torch.float32, device=c.device)
+    return _lib.home(res, y_true)
+
+
+def errors_bitwise_ber(y_true, y_pred, mask=None):
+    """Per-position bit error rate (utils.py:27-35): shape (K, 1), on ``y_true``'s device."""
+    if mask is None:
+        mask = torch.ones(y_true.size(), device=y_true.device)
+    e, m = _masked_errors(y_true, y_pred, mask)
+    return _lib.home(torch.sum(e, 0) / torch.sum(m, 0), y_true)
 
 
 def errors_bler(y_true, y_pred, get_pos=False):
-    """Block error rate (utils.py:37-51): fraction of rows with any rounded mismatch. Returns a float."""
+    """Block error rate (utils.py:37-51): fraction of rows with any rounded mismatch.
+
+    Returns ``numpy.float64`` like the reference (its loops call ``.item()`` on it, rnn_all.py:856,
+    run_models.py:331); with ``get_pos`` also the list of erroneous row indices (numpy int64)."""
+    B = y_true.shape[0]
     if get_pos:
-        t = torch.round(y_true.reshape(y_true.shape[0], -1))
-        p = torch.round(y_pred.reshape(y_pred.shape[0], -1))
-        bad = (t != p).any(dim=1)
-        return float(bad.float().mean()), list(torch.nonzero(bad).flatten().cpu().numpy())
+        e, _ = _masked_errors(y_true, y_pred, torch.ones(1, dtype=torch.float32).expand(B, 1))
+        bad = (e.reshape(B, -1).sum(1) > 0).cpu().numpy()
+        return np.float64(int(bad.sum()) * 1.0 / B), list(np.nonzero(bad.astype(int))[0])
     c = count_errors(y_true, y_pred)
-    return float(c[1].item()) / y_true.shape[0]
+    return np.float64(int(c[1].item()) * 1.0 / B)

@@ -75,12 +75,19 @@ def test_null_pointer_errors_are_reported_not_fatal():
     assert L.npd_sc_decode_soft(None, None, 1.0, 1, None, None, None, 16, None) == -1
 
 
-def test_product_path_refuses_host_tensors():
+def test_product_path_has_no_cpu_fallback():
+    """Host inputs are staged to the GPU; with no GPU visible every compute call raises."""
     import torch
-    from neural_polar_decoder_amd import NpdError, reference_polar_code
+    from neural_polar_decoder_amd import NpdError, errors_bler, reference_polar_code
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible: host tensors are staged to it")
     code = reference_polar_code(64, 32)
     with pytest.raises(NpdError):
         code.sc_decode_new(torch.zeros(4, 64), 1.0)
+    with pytest.raises(NpdError):
+        code.scl_decode(torch.zeros(4, 64), 1.0, 4)
+    with pytest.raises(NpdError):
+        errors_bler(torch.zeros(4, 8), torch.zeros(4, 8))
 
 
 def test_list_prune_select_host_utility_matches_std_nth_element(oracle):
