@@ -158,61 +158,63 @@ __device__ __noinline__ uint32_t exact_mask(const float (&km)[G], const float (&
     return nth::prune_mask(v, 2 * s, L);
 }
 
+// Surviving candidates of one group at an information leaf (pruneLists, polar.py:777-791), as a mask over
+// the list order [keep_0 .. keep_{s-1}, flip_0 .. flip_{s-1}]; m = this lane's path metric, a = |LLR|.
+template <int G>
+__device__ __forceinline__ uint32_t list_select(float m, float a, int j, int bl, int s, int L) {
+    if (2 * s <= L) return (1u << (2 * s)) - 1u;
+    float km[G], fm[G];
+    km[0] = gb<G, 0>(m, bl + 0);
+    fm[0] = km[0] + gb<G, 0>(a, bl + 0);
+    if constexpr (G > 1) {
+        km[1] = gb<G, 1>(m, bl + 1);
+        fm[1] = km[1] + gb<G, 1>(a, bl + 1);
+    }
+    if constexpr (G > 2) {
+        km[2] = gb<G, 2>(m, bl + 2);
+        fm[2] = km[2] + gb<G, 2>(a, bl + 2);
+        km[3] = gb<G, 3>(m, bl + 3);
+        fm[3] = km[3] + gb<G, 3>(a, bl + 3);
+    }
+    if constexpr (G > 4) {
+#pragma unroll
+        for (int t = 4; t < G; ++t) {
+            km[t] = __shfl(m, bl + t, 64);
+            fm[t] = km[t] + __shfl(a, bl + t, 64);
+        }
+    }
+    const float vk = m, vf = m + a;
+    int ltk = 0, lek = 0, ltf = 0, lef = 0;
+#pragma unroll
+    for (int t = 0; t < G; ++t) {
+        if (t < s) {
+            ltk += (km[t] < vk) + (fm[t] < vk);
+            lek += (km[t] <= vk) + (fm[t] <= vk);
+            ltf += (km[t] < vf) + (fm[t] < vf);
+            lef += (km[t] <= vf) + (fm[t] <= vf);
+        }
+    }
+    const bool act = j < s;
+    const bool sk = act && ltk < L;
+    const bool sf = act && ltf < L;
+    const bool st = act && ((ltk < L && lek > L) || (ltf < L && lef > L));
+    const unsigned long long bk = __ballot(sk), bf = __ballot(sf), bs = __ballot(st);
+    const uint32_t lowm = (1u << s) - 1u;
+    uint32_t msel = ((uint32_t)(bk >> bl) & lowm) | (((uint32_t)(bf >> bl) & lowm) << s);
+    if (bs) {
+        const bool mine = ((uint32_t)(bs >> bl) & ((G >= 32) ? 0xFFFFFFFFu : ((1u << G) - 1u))) != 0u;
+        if (mine) msel = exact_mask<G>(km, fm, s, L);
+    }
+    return msel;
+}
+
 template <int N, int G, int I>
 __device__ __forceinline__ void info_leaf(Lane<N, G>& c, float l, int lane) {
     const float a = __builtin_fabsf(l);
     const int L = c.L;
     const uint32_t slot = c.slot;
     const int s = slot >= 3u ? L : ((1 << slot) < L ? (1 << slot) : L);
-    const bool prune = 2 * s > L;
-    uint32_t msel;
-    if (prune) {
-        float km[G], fm[G];
-        const int bl = c.base;
-        km[0] = gb<G, 0>(c.m, bl + 0);
-        fm[0] = km[0] + gb<G, 0>(a, bl + 0);
-        if constexpr (G > 1) {
-            km[1] = gb<G, 1>(c.m, bl + 1);
-            fm[1] = km[1] + gb<G, 1>(a, bl + 1);
-        }
-        if constexpr (G > 2) {
-            km[2] = gb<G, 2>(c.m, bl + 2);
-            fm[2] = km[2] + gb<G, 2>(a, bl + 2);
-            km[3] = gb<G, 3>(c.m, bl + 3);
-            fm[3] = km[3] + gb<G, 3>(a, bl + 3);
-        }
-        if constexpr (G > 4) {
-#pragma unroll
-            for (int t = 4; t < G; ++t) {
-                km[t] = __shfl(c.m, bl + t, 64);
-                fm[t] = km[t] + __shfl(a, bl + t, 64);
-            }
-        }
-        const float vk = c.m, vf = c.m + a;
-        int ltk = 0, lek = 0, ltf = 0, lef = 0;
-#pragma unroll
-        for (int t = 0; t < G; ++t) {
-            if (t < s) {
-                ltk += (km[t] < vk) + (fm[t] < vk);
-                lek += (km[t] <= vk) + (fm[t] <= vk);
-                ltf += (km[t] < vf) + (fm[t] < vf);
-                lef += (km[t] <= vf) + (fm[t] <= vf);
-            }
-        }
-        const bool act = c.j < s;
-        const bool sk = act && ltk < L;
-        const bool sf = act && ltf < L;
-        const bool st = act && ((ltk < L && lek > L) || (ltf < L && lef > L));
-        const unsigned long long bk = __ballot(sk), bf = __ballot(sf), bs = __ballot(st);
-        const uint32_t lowm = (1u << s) - 1u;
-        msel = ((uint32_t)(bk >> bl) & lowm) | (((uint32_t)(bf >> bl) & lowm) << s);
-        if (bs) {
-            const bool mine = ((uint32_t)(bs >> bl) & ((G >= 32) ? 0xFFFFFFFFu : ((1u << G) - 1u))) != 0u;
-            if (mine) msel = exact_mask<G>(km, fm, s, L);
-        }
-    } else {
-        msel = (1u << (2 * s)) - 1u;
-    }
+    const uint32_t msel = list_select<G>(c.m, a, c.j, c.base, s, L);
     // list slot j takes the j-th surviving candidate (list order)
     uint32_t mm = msel;
 #pragma unroll
@@ -437,10 +439,326 @@ static int launch_n(const CodeParams& p, const Args& a, hipStream_t s) {
     return launch<N, 8>(p, a, s);
 }
 
+// ---------------------------------------------------------------------------------- N >= 128
+// The register file cannot hold a path's N-1 internal LLRs at N >= 128 (and a compile-time-unrolled tree
+// that large would not fit the instruction cache), so each lane's path state lives in LDS,
+// lane-interleaved (element e of lane q at dword e*64 + q: every wave access is bank-conflict free) and
+// the SC schedule is walked iteratively (leaf i: one g step at level ctz(i), f steps down to the leaf,
+// partial-sum combines for the nodes finished at i).  Per lane:
+//   LLR level d = 1..n-1 (2^d values) at rows [2^d - 2, 2^(d+1) - 2); level 0 is a register;
+//   bit rows: beta sign | beta zero | decision (u < 0) | decision (u == 0), W = N/32 words each.
+// Partial sums are values in {+-1, +-0}: the float sign bit and a zero flag reproduce the reference's
+// fp32 products exactly (sign bits XOR, zero flags OR).  The channel level is never stored: the two
+// root steps read y through L1/L2 (the G lanes of a codeword read the same row).
+// At an information leaf a lane whose slot takes another path's state copies only the LLR levels still
+// read later (level D iff leaf i is in the left child of its level-D node) and the bit rows; all lanes
+// of the wave read element e before any lane writes it (one instruction stream), so copies between
+// lanes of a group need no double buffer.
+template <int N>
+struct LdsRows {
+    static constexpr int n = log2c<N>();
+    static constexpr int W = N / 32;
+    static constexpr int kLv = N - 2;        // LLR rows
+    static constexpr int kBS = kLv;          // beta sign words
+    static constexpr int kBZ = kLv + W;      // beta zero words
+    static constexpr int kDS = kLv + 2 * W;  // decision sign words
+    static constexpr int kDZ = kLv + 3 * W;  // decision zero words
+    static constexpr int kRows = kLv + 4 * W;
+};
+
+__device__ __forceinline__ float beta_val(uint32_t sw, uint32_t zw, int b) {
+    return bitsf((((sw >> b) & 1u) << 31) | (((zw >> b) & 1u) ? 0u : 0x3f800000u));
+}
+
+template <int N, int G>
+__global__ __launch_bounds__(64) void scl_lds_kernel(const CodeParams p, const Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    using R = LdsRows<N>;
+    constexpr int n = R::n;
+    constexpr int W = R::W;
+    constexpr int T = 64 / G;
+    const int lane = threadIdx.x;
+    float* const LV = reinterpret_cast<float*>(lds_raw);
+    uint32_t* const BW = reinterpret_cast<uint32_t*>(lds_raw);
+#define LVL(row) LV[(row) * kWave + lane]
+#define BWL(row) BW[(row) * kWave + lane]
+    const int K = p.K;
+    const int L = a.L;
+    const int j = lane & (G - 1);
+    const int base = lane - j;
+    const int r = lane / G;
+    const int s_final = K >= 3 ? L : ((1 << K) < L ? (1 << K) : L);
+
+    uint32_t err_bits = 0, err_blocks = 0;
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t cw = t * T + r;
+        const int64_t cwc = cw < a.B ? cw : a.B - 1;
+        const float* yr = a.y + cwc * N;
+        const f4* y4 = reinterpret_cast<const f4*>(yr);
+#pragma unroll
+        for (int w = 0; w < 4 * W; ++w) BWL(R::kBS + w) = 0u;
+        float m = 0.0f;
+        uint32_t slot = 0;
+
+        for (int i = 0; i < N; ++i) {
+            int d;  // level the f chain starts from
+            if (i == 0) {  // left child of the root: f on the channel LLRs
+                constexpr int h = N / 2;
+                for (int q = 0; q < h / 4; ++q) {
+                    const f4 u = y4[q], v = y4[q + h / 4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) LVL(h - 2 + 4 * q + e) = f_minsum(rmul(a.scale, u[e]), rmul(a.scale, v[e]));
+                }
+                d = n - 1;
+            } else {  // right child of the node of 2^(k+1) leaves starting at i - 2^k
+                const int k = __builtin_ctz((unsigned)i);
+                const int h = 1 << k;
+                const int s0 = i - h;
+                if (k == 0) {
+                    d = 0;
+                } else if (k + 1 == n) {  // right child of the root: g on the channel LLRs
+                    for (int q = 0; q < h / 4; ++q) {
+                        const uint32_t sw = BWL(R::kBS + (q >> 3)), zw = BWL(R::kBZ + (q >> 3));
+                        const f4 u = y4[q], v = y4[q + h / 4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float b = beta_val(sw, zw, (4 * q + e) & 31);
+                            LVL(h - 2 + 4 * q + e) = b * rmul(a.scale, u[e]) + rmul(a.scale, v[e]);
+                        }
+                    }
+                    d = k;
+                } else {
+                    for (int j0 = 0; j0 < h; j0 += 32) {
+                        const int q0 = s0 + j0;
+                        const uint32_t sw = BWL(R::kBS + (q0 >> 5)) >> (q0 & 31);
+                        const uint32_t zw = BWL(R::kBZ + (q0 >> 5)) >> (q0 & 31);
+                        const int hw = h < 32 ? h : 32;
+                        for (int jj = 0; jj < hw; ++jj) {
+                            const float b = beta_val(sw, zw, jj);
+                            LVL(h - 2 + j0 + jj) = b * LVL(2 * h - 2 + j0 + jj) + LVL(2 * h - 2 + h + j0 + jj);
+                        }
+                    }
+                    d = k;
+                }
+            }
+            for (int dd = d - 1; dd >= 1; --dd) {  // left children down to level 1
+                const int h = 1 << dd;
+                for (int jj = 0; jj < h; ++jj) LVL(h - 2 + jj) = f_minsum(LVL(2 * h - 2 + jj), LVL(2 * h - 2 + h + jj));
+            }
+            float l;
+            if (d == 0) {  // leaf i is a right child: g from level 1 with the left sibling's decision
+                const uint32_t sw = BWL(R::kBS + ((i - 1) >> 5)), zw = BWL(R::kBZ + ((i - 1) >> 5));
+                l = beta_val(sw, zw, (i - 1) & 31) * LVL(0) + LVL(1);
+            } else {
+                l = f_minsum(LVL(0), LVL(1));
+            }
+
+            // ---- leaf (polar.py:805-866)
+            const bool frozen = (p.frozen[i >> 5] >> (i & 31)) & 1u;
+            const int wi = i >> 5;
+            const uint32_t bi = 1u << (i & 31);
+            if (frozen) {
+                m = m + ((l > 0.0f) ? 0.0f : __builtin_fabsf(l));  // |l| * (sign(l) != 1), polar.py:814
+                // u = +1: beta sign/zero bits stay clear
+            } else {
+                const float av = __builtin_fabsf(l);
+                const int s = slot >= 3u ? L : ((1 << slot) < L ? (1 << slot) : L);
+                float u;
+                if constexpr (G == 1) {
+                    u = sgn_bits(l);  // L = 1: plain SC with the metric tracked (pruning keeps the smaller one)
+                    const uint32_t msel = list_select<G>(m, av, j, base, s, L);
+                    if (!(msel & 1u)) {
+                        u = -u;
+                        m = m + av;
+                    }
+                } else {
+                    const uint32_t msel = list_select<G>(m, av, j, base, s, L);
+                    uint32_t mm = msel;
+#pragma unroll
+                    for (int q = 0; q < G - 1; ++q)
+                        if (q < j) mm &= mm - 1u;
+                    const int cidx = mm ? __builtin_ctz(mm) : j;
+                    const bool flip = mm ? (cidx >= s) : false;
+                    const int srcj = flip ? cidx - s : (mm ? cidx : j);
+                    const int src = base + srcj;
+                    const float ls = __shfl(l, src, 64);
+                    const float ms = __shfl(m, src, 64);
+                    if (src != lane) {
+                        // live LLR levels: D in 1..n-1 with leaf i in the left child of its level-D node
+                        for (int D = 1; D < n; ++D) {
+                            if ((i >> (D - 1)) & 1) continue;
+                            const int b0 = (1 << D) - 2;
+                            for (int e = 0; e < (1 << D); ++e) LV[(b0 + e) * kWave + lane] = LV[(b0 + e) * kWave + src];
+                        }
+#pragma unroll
+                        for (int w = 0; w < 4 * W; ++w) BW[(R::kBS + w) * kWave + lane] = BW[(R::kBS + w) * kWave + src];
+                    }
+                    u = sgn_bits(ls);
+                    if (flip) u = -u;
+                    m = flip ? ms + __builtin_fabsf(ls) : ms;
+                }
+                if (fbits(u) >> 31) BWL(R::kBS + wi) |= bi;
+                if (u == 0.0f) BWL(R::kBZ + wi) |= bi;
+                if (u < 0.0f) BWL(R::kDS + wi) |= bi;
+                if (u == 0.0f) BWL(R::kDZ + wi) |= bi;
+                slot = slot + 1u;
+            }
+            // ---- partial sums of the nodes whose right child ends at leaf i (the right spine is never read)
+            if (i != N - 1) {
+                for (int l2 = 0; (i >> l2) & 1; ++l2) {
+                    const int h = 1 << l2;
+                    const int s0 = i + 1 - 2 * h;
+                    if (h < 32) {
+                        const int w = s0 >> 5, o = s0 & 31;
+                        const uint32_t lowm = (1u << h) - 1u;
+                        uint32_t sw = BWL(R::kBS + w), zw = BWL(R::kBZ + w);
+                        sw ^= ((sw >> (o + h)) & lowm) << o;
+                        zw |= ((zw >> (o + h)) & lowm) << o;
+                        BWL(R::kBS + w) = sw;
+                        BWL(R::kBZ + w) = zw;
+                    } else {
+                        const int w0 = s0 >> 5, hw = h >> 5;
+                        for (int q = 0; q < hw; ++q) {
+                            BWL(R::kBS + w0 + q) ^= BWL(R::kBS + w0 + hw + q);
+                            BWL(R::kBZ + w0 + q) |= BWL(R::kBZ + w0 + hw + q);
+                        }
+                    }
+                }
+            }
+        }
+
+        // ---- ML choice (polar.py:868-874): codeword of each path from its decision bits
+        uint32_t S[W], Z[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            S[w] = BWL(R::kDS + w);
+            Z[w] = BWL(R::kDZ + w);
+        }
+        constexpr uint32_t kLow[5] = {0x55555555u, 0x33333333u, 0x0F0F0F0Fu, 0x00FF00FFu, 0x0000FFFFu};
+#pragma unroll
+        for (int dd = 0; dd < 5; ++dd) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                S[w] ^= (S[w] >> (1 << dd)) & kLow[dd];
+                Z[w] |= (Z[w] >> (1 << dd)) & kLow[dd];
+            }
+        }
+#pragma unroll
+        for (int dd = 5; dd < n; ++dd) {
+            const int st = 1 << (dd - 5);
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                if ((w & st) == 0) {
+                    S[w] ^= S[w + st];
+                    Z[w] |= Z[w + st];
+                }
+            }
+        }
+        float dist = 0.0f;
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q) {
+            const f4 v = y4[q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = 4 * q + e;
+                const uint32_t sb = (S[k >> 5] >> (k & 31)) & 1u, zb = (Z[k >> 5] >> (k & 31)) & 1u;
+                const float cv = zb ? 0.0f : (sb ? -1.0f : 1.0f);
+                const float dd = cv - v[e];
+                dist = dist + rmul(dd, dd);
+            }
+        }
+        float bd = j < s_final ? dist : __builtin_inff();
+        int bj = j;
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const float od = __shfl_xor(bd, off, 64);
+            const int oj = __shfl_xor(bj, off, 64);
+            if (od < bd || (od == bd && oj < bj)) {
+                bd = od;
+                bj = oj;
+            }
+        }
+        if (j == bj && cw < a.B) {
+            uint32_t e = 0;
+            uint32_t mw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            if (a.count) {
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    if (blk * 128 < K) {
+                        const u32x4 o = philox_block(a.seed, kStreamMsg, a.cw_offset + (uint64_t)cw, (uint32_t)blk);
+                        mw[4 * blk + 0] = o.x;
+                        mw[4 * blk + 1] = o.y;
+                        mw[4 * blk + 2] = o.z;
+                        mw[4 * blk + 3] = o.w;
+                    }
+                }
+            }
+            float* mrow = a.msg ? a.msg + cw * K : nullptr;
+            for (int k = 0; k < K; ++k) {
+                const int pos = p.info[k];
+                const uint32_t sb = (BWL(R::kDS + (pos >> 5)) >> (pos & 31)) & 1u;
+                const uint32_t zb = (BWL(R::kDZ + (pos >> 5)) >> (pos & 31)) & 1u;
+                if (mrow) mrow[k] = zb ? 0.0f : (sb ? -1.0f : 1.0f);
+                e += ((sb ^ ((mw[k >> 5] >> (k & 31)) & 1u)) | zb);
+            }
+            if (a.uhat) {
+                float* urow = a.uhat + cw * N;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    const uint32_t sb = (BWL(R::kDS + (k >> 5)) >> (k & 31)) & 1u;
+                    const uint32_t zb = (BWL(R::kDZ + (k >> 5)) >> (k & 31)) & 1u;
+                    urow[k] = zb ? 0.0f : (sb ? -1.0f : 1.0f);
+                }
+            }
+            err_bits += e;
+            err_blocks += e ? 1u : 0u;
+        }
+    }
+#undef LVL
+#undef BWL
+    if (a.count) {
+        const uint32_t eb = wave_sum_u32(err_bits);
+        const uint32_t bl = wave_sum_u32(err_blocks);
+        if (lane == 0) {
+            atomicAdd(a.counters + 0, (unsigned long long)eb);
+            atomicAdd(a.counters + 1, (unsigned long long)bl);
+        }
+    }
+}
+
+template <int N, int G>
+static int launch_lds(const CodeParams& p, Args a, hipStream_t s) {
+    constexpr int T = 64 / G;
+    const size_t lds = (size_t)LdsRows<N>::kRows * kWave * sizeof(float);
+    a.ntiles = (a.B + T - 1) / T;
+    auto kern = scl_lds_kernel<N, G>;
+    static bool attr_set = false;  // benign race (idempotent)
+    if (!attr_set && lds > 65536) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr_set = true;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, p, a);
+    return launch_check("scl_lds_kernel launch");
+}
+
+template <int N>
+static int launch_lds_n(const CodeParams& p, const Args& a, hipStream_t s) {
+    if (a.L == 1) return launch_lds<N, 1>(p, a, s);
+    if (a.L == 2) return launch_lds<N, 2>(p, a, s);
+    if (a.L <= 4) return launch_lds<N, 4>(p, a, s);
+    return launch_lds<N, 8>(p, a, s);
+}
+
 static int run(const npd_code* code, Args& a, hipStream_t s) {
     const CodeParams& p = code->p;
     if (p.pac) return fail(NPD_ENOTSUP, "scl_decode: the reference defines SC-List for Polar codes only");
-    if (p.N < 8 || p.N > 64) return fail(NPD_ENOTSUP, "scl_decode: N must be 8..64 in this build");
+    if (p.N < 8 || p.N > 256) return fail(NPD_ENOTSUP, "scl_decode: N must be 8..256");
     if (a.L < 1 || a.L > 8) return fail(NPD_EINVAL, "scl_decode: list size must be 1..8");
     if ((((uintptr_t)a.y) & 15) != 0) return fail(NPD_EINVAL, "scl_decode: y must be 16-byte aligned");
     if (a.B == 0) return NPD_OK;
@@ -448,7 +766,9 @@ static int run(const npd_code* code, Args& a, hipStream_t s) {
         case 8: return launch_n<8>(p, a, s);
         case 16: return launch_n<16>(p, a, s);
         case 32: return launch_n<32>(p, a, s);
-        default: return launch_n<64>(p, a, s);
+        case 64: return launch_n<64>(p, a, s);
+        case 128: return launch_lds_n<128>(p, a, s);
+        default: return launch_lds_n<256>(p, a, s);
     }
 }
 

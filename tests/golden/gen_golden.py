@@ -164,10 +164,10 @@ def tie_rows(N, rng, count):
     return grid[rng.integers(0, grid.size, (count, N))]
 
 
-def gen_scl():
-    rng = np.random.default_rng(8)
-    for N, K, L, per in [(64, 32, 4, 48), (32, 16, 4, 64), (16, 8, 2, 64), (64, 32, 8, 24), (32, 16, 1, 64),
-                         (32, 16, 3, 48), (8, 4, 4, 64)]:
+def gen_scl(cases=None, seed=8):
+    rng = np.random.default_rng(seed)
+    for N, K, L, per in cases or [(64, 32, 4, 48), (32, 16, 4, 64), (16, 8, 2, 64), (64, 32, 8, 24), (32, 16, 1, 64),
+                                  (32, 16, 3, 48), (8, 4, 4, 64)]:
         code = polar_code(N, K)
         torch.manual_seed(2000 + N + K + L)
         ys, snrs, leafs, hats = [], [], [], []
@@ -183,6 +183,11 @@ def gen_scl():
             hats.append(hat.numpy())
         save(f"scl_{N}_{K}_L{L}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), leaf=np.concatenate(leafs),
              msg_hat=np.concatenate(hats), info=np.asarray(code.info_positions, np.int64), L=np.int64(L))
+
+
+def gen_scl_long():
+    """SC-List at the lengths the C5 eval loop decodes (testXformer, run_models.py:329: L=4 at N=256)."""
+    gen_scl([(128, 64, 4, 16), (256, 128, 4, 8), (128, 64, 8, 8)], seed=9)
 
 
 def gen_lse():
@@ -368,6 +373,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "lse", "lse_soft", "pac", "errors", "gru", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "pac", "errors", "gru", "conv"]
     for w in which:
         globals()["gen_" + w]()

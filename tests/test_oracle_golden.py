@@ -129,7 +129,7 @@ def test_oracle_mc_is_generate_then_decode(oracle):
 
 
 SCL_FIXTURES = ["scl_64_32_L4", "scl_32_16_L4", "scl_16_8_L2", "scl_64_32_L8", "scl_32_16_L1", "scl_32_16_L3",
-                "scl_8_4_L4"]
+                "scl_8_4_L4", "scl_128_64_L4", "scl_256_128_L4", "scl_128_64_L8"]
 
 
 @pytest.mark.parametrize("name", SCL_FIXTURES)

@@ -14,7 +14,7 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 SCL_FIXTURES = ["scl_64_32_L4", "scl_32_16_L4", "scl_16_8_L2", "scl_64_32_L8", "scl_32_16_L1", "scl_32_16_L3",
-                "scl_8_4_L4"]
+                "scl_8_4_L4", "scl_128_64_L4", "scl_256_128_L4", "scl_128_64_L8"]
 
 
 def polar_for(N, info):
@@ -39,7 +39,7 @@ def test_scl_decode_golden(name):
         assert np.array_equal(leaf.cpu().numpy(), d["leaf"][m]), (name, s)
 
 
-@pytest.mark.parametrize("N,K", [(64, 32), (32, 16), (16, 8), (8, 4), (64, 22)])
+@pytest.mark.parametrize("N,K", [(64, 32), (32, 16), (16, 8), (8, 4), (64, 22), (128, 64), (256, 128), (256, 200)])
 @pytest.mark.parametrize("L", [1, 2, 3, 4, 5, 8])
 def test_scl_vs_oracle_random(oracle, N, K, L):
     """Ragged batches (not a multiple of the 64/G codewords of a wave tile) vs the oracle."""
@@ -60,7 +60,7 @@ def test_scl_tie_heavy_vs_oracle(oracle):
     from neural_polar_decoder_amd import reference_polar_code
     rng = np.random.default_rng(11)
     grid = np.array([-1.5, -1.0, -0.5, 0.0, 0.5, 1.0, 1.5], np.float32)
-    for N, K, L in [(64, 32, 4), (32, 16, 8), (16, 8, 3), (64, 32, 2)]:
+    for N, K, L in [(64, 32, 4), (32, 16, 8), (16, 8, 3), (64, 32, 2), (128, 64, 4), (256, 128, 4), (256, 128, 8)]:
         code = reference_polar_code(N, K)
         y = grid[rng.integers(0, grid.size, (1000, N))]
         _, hat = code.scl_decode(t(y), 1.0, L, want_llrs=False)
@@ -68,15 +68,17 @@ def test_scl_tie_heavy_vs_oracle(oracle):
         assert np.array_equal(hat.cpu().numpy(), oh), (N, K, L)
 
 
-@pytest.mark.parametrize("L", [2, 4, 8])
-def test_scl_decode_mc_counters_exact(oracle, L):
+@pytest.mark.parametrize("N,K,L", [(64, 32, 2), (64, 32, 4), (64, 32, 8), (256, 128, 4), (256, 200, 2), (128, 64, 8)])
+def test_scl_decode_mc_counters_exact(oracle, N, K, L):
+    """Fused error counting (message bits regenerated from Philox in the kernel; K > 128 uses a second
+    Philox block) equals the oracle's count on the oracle's own decisions."""
     from neural_polar_decoder_amd import reference_polar_code
-    code = reference_polar_code(64, 32)
-    B, seed, off = 3000, 9, 4242
+    code = reference_polar_code(N, K)
+    B, seed, off = 3000 if N <= 64 else 1000, 9, 4242
     for si, snr in enumerate([1.0, 3.0]):
         msg, _, y = code.mc_generate(B, snr, seed, si, off)
         cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
-        hat = torch.empty(B, 32, device=DEV)
+        hat = torch.empty(B, K, device=DEV)
         code.scl_decode_mc(y, snr, L, seed, off, cnt, msg_hat=hat)
         _, oh, _ = oracle.scl_decode(y.cpu().numpy(), snr, code.info_positions, L)
         assert np.array_equal(hat.cpu().numpy(), oh)
@@ -97,6 +99,22 @@ def test_scl_list_gain_and_noiseless():
     code.scl_decode_mc(y, 2.0, 4, 3, 0, c_l4)
     bler_sc, bler_l4 = c_sc[1].item() / B, c_l4[1].item() / B
     assert bler_l4 < 0.8 * bler_sc, (bler_sc, bler_l4)
+
+
+def test_scl_long_noiseless_and_list_gain():
+    """N = 256 (the C5 eval loop's SC-List, run_models.py:329): noiseless words decode exactly, and L = 4
+    beats SC on the same received words."""
+    from neural_polar_decoder_amd import reference_polar_code
+    code = reference_polar_code(256, 128)
+    B = 1 << 14
+    msg, x, y = code.mc_generate(B, 1.5, seed=7, want_x=True)
+    _, hat = code.scl_decode(x, 1.5, 4, want_llrs=False)
+    assert torch.equal(hat, msg)
+    c_sc = torch.zeros(2, dtype=torch.int64, device=DEV)
+    c_l4 = torch.zeros(2, dtype=torch.int64, device=DEV)
+    code.sc_decode_mc(y, 1.5, 7, 0, c_sc)
+    code.scl_decode_mc(y, 1.5, 4, 7, 0, c_l4)
+    assert c_l4[1].item() < 0.8 * c_sc[1].item(), (c_sc.tolist(), c_l4.tolist())
 
 
 def test_scl_montecarlo_shard_invariance():
