@@ -1,13 +1,29 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Polar(64,32) SC decoding on MI355X (BASELINE.json configs[1]).
+"""Headline benchmark: Polar(64,32) SC decoding on MI355X (BASELINE.json configs[1]), plus the other
+configs' legs and the combined SC + CRISP-GRU eval step the metric string names.
 
-One "step" = SC-decode one batch of B = 2^20 received words per SNR point for the SNR sweep
-0,1,2,3,4 dB (one launch of the fused decode + BER/BLER-count kernel; y already resident in HBM,
-msg_hat (B,K) fp32 written back, error counters accumulated on device).
+``value`` -- one "step" = SC-decode one batch of B = 2^20 received words per SNR point for the SNR
+sweep 0,1,2,3,4 dB per GPU (one launch of the fused decode + BER/BLER-count kernel; y resident in
+HBM before timing, msg_hat (B,K) fp32 written back, error counters accumulated on device).
+
+Secondary legs (same JSON line; every leg runs on every rank over its own codeword shard, is timed
+between barriers and reports the max over ranks; whole-job codewords/s):
+  montecarlo      the Monte-Carlo step itself: Philox message -> encode -> AWGN -> SC -> count, all
+                  SNR points, y never stored (fused kernel)
+  sc_plus_gru     the metric as named: the eval step of rnn_all.py:853-880 on the same words -- SC and
+                  CRISP GRU (hidden 64, 2 layers) both decode every word of the sweep (configs[1]+[2])
+  crisp_gru       configs[2]: GRU decode alone, B = 2^20, fp32 (plus opt-in bf16x3 / bf16 kernels)
+  pac_gru         configs[3]: PAC(128,64) CRISP GRU, 2^20 codewords per GPU (2^23 at 8 GPUs), RCCL
+                  all-reduce of the BER/BLER counters
+  pac_sc          PAC(128,64) SC decoding (the configs[3] eval's SC baseline, rnn_all.py:696)
+  conv_model      configs[4]: Polar(256,128) convNet (embed 128), fp32 MFMA
+  scl             SC-List L = 4, 8 at Polar(64,32) and L = 4 at Polar(256,128) (run_models.py:329)
+  sc_lse          exact-LSE SC (polar.py:209-279)
 
   python bench.py [--gpus N --steps K --warmup W]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU;
-  each rank decodes its own codeword range -> weak scaling; one all-reduce of the counters at the end)
+  --gpus N > 1 without a launcher: bench.py starts `python -m torch.distributed.run --nproc-per-node N`
+  on itself (the parent never touches the GPU) and exits with its status.  Under a launcher,
+  WORLD_SIZE must equal --gpus.
 
 Prints ONE JSON line (rank 0).  The roofline leg times every decode launch with HIP events on the
 stream the kernel runs on; the cpu_baseline leg times the CPU oracle (oracle/, a bit-exact C
@@ -18,6 +34,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,10 +48,16 @@ sys.path.insert(0, ROOT)
 N_CODE, K_CODE = 64, 32
 BYTES_PER_CW = 4 * N_CODE + 4 * K_CODE  # y in + msg_hat out
 HBM_PEAK_GBS = 8000.0                    # MI355X spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy
+FP32_PEAK_TF = 157.3                     # MI355X fp32 vector / fp32 MFMA (MI355X_MICROARCH.md)
 SEED = 1234
 # reference sc_decode_new anchors (1e5 codewords per SNR, torch RNG)
 ANCHORS = {0.0: (1.944e-1, 5.664e-1), 1.0: (9.996e-2, 3.166e-1), 2.0: (3.634e-2, 1.248e-1),
            3.0: (8.425e-3, 3.116e-2), 4.0: (1.258e-3, 4.910e-3)}
+
+
+def gru_flop_per_cw(N, F):
+    """y.W_ih once + per step the two layers' gate GEMVs and the output dot."""
+    return 2 * 3 * F * N + N * (2 * 3 * F * F + 2 * 2 * 3 * F * F + 2 * F)
 
 
 def parse():
@@ -45,16 +69,35 @@ def parse():
     ap.add_argument("--snrs", type=str, default="0,1,2,3,4")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gru", action="store_true", help="skip the secondary CRISP-GRU measurement")
+    ap.add_argument("--no-gru", action="store_true", help="skip the GRU legs (sc_plus_gru, crisp_gru, pac_gru)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
-    ap.add_argument("--no-conv", action="store_true", help="skip the secondary conv-model measurement")
-    ap.add_argument("--no-scl", action="store_true", help="skip the secondary SC-List measurement")
-    ap.add_argument("--no-lse", action="store_true", help="skip the secondary exact-LSE SC measurement")
+    ap.add_argument("--no-conv", action="store_true", help="skip the conv-model leg")
+    ap.add_argument("--no-scl", action="store_true", help="skip the SC-List leg")
+    ap.add_argument("--no-lse", action="store_true", help="skip the exact-LSE SC leg")
+    ap.add_argument("--no-mc", action="store_true", help="skip the fused Monte-Carlo leg")
+    ap.add_argument("--no-pac", action="store_true", help="skip the PAC(128,64) SC leg")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
-def dist_setup(args):
+# ------------------------------------------------------------------------------- launch / distributed
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args):
+    """--gpus N > 1 with no launcher: one rank per GPU through torch.distributed.run, as a child process
+    (this process has not initialised HIP and never does)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -63,6 +106,8 @@ def dist_setup(args):
         torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != world:
+            raise SystemExit(f"RCCL world size {dist.get_world_size()} != WORLD_SIZE {world}")
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -81,11 +126,66 @@ def allreduce(t, op, world):
     return t
 
 
+def _max():
+    import torch.distributed as dist
+    return dist.ReduceOp.MAX
+
+
+def _sum():
+    import torch.distributed as dist
+    return dist.ReduceOp.SUM
+
+
+class Timer:
+    """Barrier + synchronize on both sides of `iters` calls of fn; seconds per call, max over ranks."""
+
+    def __init__(self, world, dev):
+        self.world, self.dev = world, dev
+
+    def __call__(self, fn, iters=1, warm=1):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize()
+        barrier(self.world)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        barrier(self.world)
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.dev)
+        return float(allreduce(el, _max(), self.world).item()) / iters
+
+
+def event_ms(fn, iters, stream):
+    """Average per-call device time of fn by HIP events recorded on the stream the kernels run on."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record(stream)
+    for _ in range(iters):
+        fn()
+    e.record(stream)
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+# ------------------------------------------------------------------------------------ CPU baseline
+def available_cores():
+    """Cores this process may use: the affinity set, capped by a cgroup CPU quota when one is set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(-(-int(q) // int(p)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(ys_host, snrs, info, budget_s):
     """Oracle (bit-exact C restatement of sc_decode_new) on the host cores, timed over repeated passes
     of a bounded sample of the same received words until ~budget_s seconds of CPU work are done."""
     from oracle import oracle as O
-    threads = min(len(os.sched_getaffinity(0)), 16)
+    threads = available_cores()
     O.set_num_threads(threads)
     O.sc_decode(ys_host[0][:4096], snrs[0], info)  # warm
     done, passes = 0, 0
@@ -108,37 +208,77 @@ def cpu_baseline(ys_host, snrs, info, budget_s):
     except OSError:
         pass
     return {"value": done / el, "unit": "codewords/s", "cores": threads, "kind": "port",
-            "sample": f"oracle sc_decode (C, OpenMP, {threads} threads, {cpu}): {passes} passes over the first "
-                      f"{ys_host[0].shape[0]} received words of each of {len(snrs)} SNR points "
-                      f"({done} codewords, {el:.1f} s)",
+            "sample": f"oracle sc_decode (C, OpenMP, {threads} threads = all cores of the affinity set / cgroup "
+                      f"quota, {cpu}): {passes} passes over the first {ys_host[0].shape[0]} received words of "
+                      f"each of {len(snrs)} SNR points ({done} codewords, {el:.1f} s)",
             "reference_measured_8core": 4.67e3}
 
 
-def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
-    """Secondary line (configs[2]): CRISP GRU hidden 64, 2 layers, Polar(64,32), fused decode kernel.
-    Seeded random weights (no trained checkpoint ships with the reference). The fp32 kernel (the
-    reference's arithmetic) is the line's value; the opt-in bf16x3 / bf16 MFMA kernels are timed
-    beside it with their decision agreement against the fp32 path on the same batch."""
-    from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
-    torch.manual_seed(0)
-    net = RNN_Model("GRU", N_CODE + 2, 64, 1, 2, N_CODE, 0, 0).to(dev)
-    yb = y[:batch].contiguous()
-    F, N = 64, N_CODE
-    flop_cw = 2 * 3 * F * N + N * (2 * 3 * F * F + 2 * 2 * 3 * F * F + 2 * F)  # SURVEY.md 8(d): 4.751 MFLOP
+# ------------------------------------------------------------------------------------ secondary legs
+def mc_leg(code, snrs, B, cw0, world, timer, dev, ref_counts):
+    """The Monte-Carlo step: message -> encode -> AWGN -> SC -> count for every SNR point, y never
+    stored (npd_sc_mc_sweep_fused).  Counts must equal the decode-only leg's on the same words."""
+    cnt = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        code.sc_mc_sweep_fused(B, snrs, SEED, cw0, cnt)
+
+    step()
+    torch.cuda.synchronize()
+    one = cnt.clone()
+    cnt.zero_()
+    t = timer(step, iters=5, warm=1)
+    ms = event_ms(step, 3, stream)
+    allreduce(one, _sum(), world)
+    return {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
+            "avg_launch_ms": ms, "counts_equal_decode_leg": bool(torch.equal(one.cpu(), ref_counts)),
+            "bound": "VALU (Philox + Box-Muller + SC per codeword; no HBM traffic besides counters)",
+            "config": "Polar(64,32), 2^20 codewords per SNR per GPU, 0-4 dB, one fused launch per sweep"}
+
+
+def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg):
+    """The eval step the metric names (rnn_all.py:853-880): SC and CRISP GRU decode the same words at
+    every SNR point and both are counted."""
+    from neural_polar_decoder_amd.montecarlo import seeded_crisp
+    from neural_polar_decoder_amd.utils import count_errors
+    net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev)
+    info = torch.as_tensor(np.asarray(code.info_positions), device=dev)
+    c_sc = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    c_gru = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+
+    def step():
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc)
+        for si in range(len(snrs)):
+            count_errors(msg, dec.decode(net, False, yall[si]).index_select(1, info), c_gru[si])
+
+    t = timer(step, iters=2, warm=1)
+    allreduce(c_gru, _sum(), world)
+    n = 3 * world * B
+    cg = c_gru.cpu().numpy()
+    return {"value": world * len(snrs) * B / t, "unit": "codewords/s (each decoded by SC and by the GRU)",
+            "ms_per_step": t * 1e3,
+            "gru_ber": {str(s): float(cg[i, 0]) / (n * K_CODE) for i, s in enumerate(snrs)},
+            "gru_bler": {str(s): float(cg[i, 1]) / n for i, s in enumerate(snrs)},
+            "config": "configs[1]+[2]: Polar(64,32), 2^20 words per SNR per GPU, 0-4 dB; SC sweep launch + 5 CRISP "
+                      "GRU (hidden 64, 2 layers, fp32, seeded untrained weights) decodes + device counts"}
+
+
+def gru_leg(code, dev, y, B, world, timer):
+    """configs[2]: CRISP GRU hidden 64, 2 layers, Polar(64,32), B = 2^20, fused decode kernel.  The fp32
+    kernel (the reference's arithmetic) is the value; the opt-in bf16x3 / bf16 MFMA kernels are timed
+    beside it with their decision agreement against fp32 on the same words."""
+    from neural_polar_decoder_amd.montecarlo import seeded_crisp
+    flop_cw = gru_flop_per_cw(N_CODE, 64)
+    stream = torch.cuda.current_stream(dev)
     res, ref_dec = {}, None
-    for prec, peak in (("fp32", 157.3), ("bf16x3", 2516.6), ("bf16", 2516.6)):
-        dec = RNN_decoder("y_input", N_CODE, code.info_positions, onehot=True, precision=prec)
-        d0 = dec.decode(net, False, yb)  # warm (weights packed once)
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(iters):
-            dec.decode(net, False, yb)
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / iters
-        tflops = flop_cw * batch / (ms / 1e3) / 1e12
-        r = {"value": batch / (ms / 1e3), "avg_launch_ms": ms, "achieved_tflops": tflops, "peak_tflops": peak,
+    for prec, peak in (("fp32", FP32_PEAK_TF), ("bf16x3", 2516.6), ("bf16", 2516.6)):
+        net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev, precision=prec)
+        d0 = dec.decode(net, False, y)
+        t = timer(lambda: dec.decode(net, False, y), iters=2, warm=0)
+        ms = event_ms(lambda: dec.decode(net, False, y), 2, stream)
+        tflops = flop_cw * B / (ms / 1e3) / 1e12
+        r = {"value": world * B / t, "avg_launch_ms": ms, "achieved_tflops": tflops, "peak_tflops": peak,
              "frac": tflops / peak}
         if ref_dec is None:
             ref_dec = d0
@@ -146,85 +286,137 @@ def gru_measure(code, dev, y, snr, batch=1 << 18, iters=3):
             r["cw_agreement_vs_fp32"] = (d0 == ref_dec).all(1).float().mean().item()
         res[prec] = r
     f = res["fp32"]
-    return {"value": f["value"], "unit": "codewords/s", "batch": batch, "avg_launch_ms": f["avg_launch_ms"],
+    return {"value": f["value"], "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": f["avg_launch_ms"],
             "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "algorithmic_flop_per_cw": flop_cw,
-            "achieved_tflops": f["achieved_tflops"], "peak_tflops_fp32": 157.3, "frac": f["frac"],
+            "achieved_tflops": f["achieved_tflops"], "peak_tflops_fp32": FP32_PEAK_TF, "frac": f["frac"],
             "bf16x3": res["bf16x3"], "bf16": res["bf16"],
-            "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input"}
+            "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input, 2 dB, 2^20 per GPU"}
 
 
-KERNEL_NAME = "sc_fast_kernel<64>"
+def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
+    """configs[3]: PAC(128,64) (RM profile, g = 91), 2^20 codewords per GPU per SNR (2^23 over 8 GPUs),
+    received words resident; CRISP GRU hidden 64 and PAC SC; one RCCL all-reduce of the counters."""
+    import argparse as _ap
+    from neural_polar_decoder_amd import PAC
+    from neural_polar_decoder_amd.montecarlo import seeded_crisp
+    from neural_polar_decoder_amd.utils import count_errors
+    code = PAC(_ap.Namespace(target_K=64), 128, 64, 91)
+    cw0 = rank * B
+    info = torch.as_tensor(np.asarray(code.B), device=dev)
+    ys, msg = [], None
+    for si, snr in enumerate(snrs):
+        m, _, y = code.mc_generate(B, snr, SEED, si, cw0, device=dev, want_msg=msg is None)
+        msg = m if msg is None else msg
+        ys.append(y)
+    out = {}
+    stream = torch.cuda.current_stream(dev)
+    if do_sc:
+        c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+
+        def sc_step():
+            for si, snr in enumerate(snrs):
+                code.sc_decode_mc(ys[si], snr, SEED, cw0, c[si])
+
+        t = timer(sc_step, iters=3, warm=1)
+        ms = event_ms(lambda: code.sc_decode_mc(ys[2], snrs[2], SEED, cw0, c[2]), 3, stream)
+        c.zero_()
+        sc_step()
+        allreduce(c, _sum(), world)
+        cc = c.cpu().numpy()
+        nb = 768 * B  # 4N + 4K bytes per codeword (SURVEY.md 8(d))
+        out["pac_sc"] = {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
+                         "avg_launch_ms": ms, "roofline": {"bound": "hbm", "achieved_gbs": nb / (ms / 1e3) / 1e9,
+                                                           "peak_gbs": HBM_PEAK_GBS,
+                                                           "frac": nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                         "ber": {str(s): float(cc[i, 0]) / (world * B * 64) for i, s in enumerate(snrs)},
+                         "bler": {str(s): float(cc[i, 1]) / (world * B) for i, s in enumerate(snrs)},
+                         "config": "PAC(128,64) SC (pac_sc_decode, pac_code.py:534-573), 2^20 per SNR per GPU, 0-4 dB"}
+    if do_gru:
+        net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev)
+        c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+
+        def gru_step():
+            for si in range(len(snrs)):
+                count_errors(msg, dec.decode(net, False, ys[si]).index_select(1, info), c[si])
+
+        t = timer(gru_step, iters=1, warm=0)
+        ms = event_ms(lambda: dec.decode(net, False, ys[2]), 1, stream)
+        allreduce(c, _sum(), world)  # the RCCL BER reduce of configs[3]
+        cc = c.cpu().numpy()
+        n = world * B  # counted once per SNR (the timer's single call); the event pass does not count
+        flop_cw = gru_flop_per_cw(128, 64)
+        tf = flop_cw * B / (ms / 1e3) / 1e12
+        out["pac_gru"] = {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
+                          "avg_launch_ms": ms, "algorithmic_flop_per_cw": flop_cw, "achieved_tflops": tf,
+                          "peak_tflops_fp32": FP32_PEAK_TF, "frac": tf / FP32_PEAK_TF,
+                          "total_codewords": world * len(snrs) * B,
+                          "ber": {str(s): float(cc[i, 0]) / (n * 64) for i, s in enumerate(snrs)},
+                          "bler": {str(s): float(cc[i, 1]) / n for i, s in enumerate(snrs)},
+                          "config": "configs[3]: PAC(128,64) CRISP GRU hidden 64, 2 layers, fp32, seeded untrained "
+                                    "weights; 2^20 per SNR per GPU (2^23 at 8 GPUs), 0-4 dB, RCCL counter all-reduce"}
+    return out
 
 
-def scl_measure(code, dev, y, snr, batch=1 << 18, iters=3):
-    """Secondary line: SC-List, Polar(64,32), list sizes 4 and 8, decode + fused
-    counts (npd_scl_decode_mc) on the configs[1] received words at 2 dB."""
-    yb = y[:batch].contiguous()
+def scl_leg(code64, dev, y64, snr, world, timer):
+    """SC-List: Polar(64,32) L = 4, 8 and Polar(256,128) L = 4 (the C5 eval's per-batch call,
+    run_models.py:329); decode + fused counts (npd_scl_decode_mc)."""
+    from neural_polar_decoder_amd import reference_polar_code
+    stream = torch.cuda.current_stream(dev)
+    B = 1 << 18
+    yb = y64[:B].contiguous()
     cnt = torch.zeros(2, dtype=torch.int64, device=dev)
     res = {}
     for L in (4, 8):
-        code.scl_decode_mc(yb, snr, L, SEED, 0, cnt)
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(iters):
-            code.scl_decode_mc(yb, snr, L, SEED, 0, cnt)
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / iters
-        res[f"L{L}"] = {"value": batch / (ms / 1e3), "avg_launch_ms": ms}
-    return {"value": res["L4"]["value"], "unit": "codewords/s", "list_size": 4, "batch": batch,
-            "avg_launch_ms": res["L4"]["avg_launch_ms"], "L8": res["L8"],
-            "bound": "VALU/LDS (per-path SC + list bookkeeping; 384 B/cw of HBM traffic is not the limit)",
-            "config": "Polar(64,32) scl_decode(L) (polar.py:793-876), 2 dB, decode + fused BER/BLER counts"}
+        t = timer(lambda: code64.scl_decode_mc(yb, snr, L, SEED, 0, cnt), iters=3, warm=1)
+        res[f"N64_L{L}"] = {"value": world * B / t, "avg_launch_ms": event_ms(
+            lambda: code64.scl_decode_mc(yb, snr, L, SEED, 0, cnt), 2, stream)}
+    c256 = reference_polar_code(256, 128)
+    B2 = 1 << 16
+    _, _, y2 = c256.mc_generate(B2, 1.0, SEED, 0, 0, device=dev, want_msg=False)
+    t = timer(lambda: c256.scl_decode_mc(y2, 1.0, 4, SEED, 0, cnt), iters=2, warm=1)
+    res["N256_L4"] = {"value": world * B2 / t, "avg_launch_ms": event_ms(
+        lambda: c256.scl_decode_mc(y2, 1.0, 4, SEED, 0, cnt), 1, stream), "batch_per_gpu": B2}
+    return {"value": res["N64_L4"]["value"], "unit": "codewords/s", "list_size": 4, "batch_per_gpu": B,
+            "avg_launch_ms": res["N64_L4"]["avg_launch_ms"], "L8": res["N64_L8"], "polar_256_128_L4": res["N256_L4"],
+            "bound": "VALU/LDS (per-path SC + list bookkeeping; HBM traffic is not the limit)",
+            "config": "scl_decode(L) (polar.py:793-876), Polar(64,32) at 2 dB and Polar(256,128) at 1 dB, "
+                      "decode + fused BER/BLER counts"}
 
 
-def lse_measure(code, dev, y, snr, batch=1 << 18, iters=2):
-    """Secondary line: exact-LSE SC (PolarCode.sc_decode, polar.py:209-279),
-    Polar(64,32) at 2 dB, hard and soft decisions, msg_hat out.  Transcendental-bound (4 exp/log per
-    check node, 192 check nodes per codeword)."""
-    yb = y[:batch].contiguous()
+def lse_leg(code, dev, y, snr, world, timer):
+    """exact-LSE SC (PolarCode.sc_decode, polar.py:209-279), Polar(64,32) at 2 dB, hard and soft,
+    msg_hat out.  Transcendental-bound (4 exp/log per check node, 192 check nodes per codeword)."""
+    B = 1 << 18
+    yb = y[:B].contiguous()
     res = {}
     for tag, hard in (("hard", True), ("soft", False)):
-        code.sc_decode(yb, snr, hard_decision=hard)
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(iters):
-            code.sc_decode(yb, snr, hard_decision=hard)
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / iters
-        res[tag] = {"value": batch / (ms / 1e3), "avg_launch_ms": ms}
-    return {"value": res["soft"]["value"], "unit": "codewords/s", "batch": batch, "soft": res["soft"],
+        t = timer(lambda: code.sc_decode(yb, snr, hard_decision=hard), iters=2, warm=1)
+        res[tag] = {"value": world * B / t}
+    return {"value": res["soft"]["value"], "unit": "codewords/s", "batch_per_gpu": B, "soft": res["soft"],
             "hard": res["hard"], "bound": "transcendental VALU (exp/log per check node)",
             "config": "Polar(64,32) sc_decode exact-LSE (polar.py:209-279), 2 dB, msg_hat out"}
 
 
-def conv_measure(dev, batch=8192, iters=3):
-    """Secondary line (configs[4], per GPU): Polar(256,128) convNet decoder, embed 128 (run_alt.sh),
-    seeded random weights, fp32 MFMA kernels."""
-    import argparse as _ap
+def conv_leg(dev, rank, world, timer, batch=8192):
+    """configs[4]: Polar(256,128) convNet decoder, embed 128 (run_alt.sh), seeded random weights, fp32
+    MFMA kernels; batch per GPU, whole-job codewords/s."""
     from neural_polar_decoder_amd import reference_polar_code
-    from neural_polar_decoder_amd.models import convNet
-    torch.manual_seed(0)
-    net = convNet(_ap.Namespace(embed_dim=128, max_len=256, N=256, dont_use_bias=False, dropout=0.0)).to(dev).eval()
+    from neural_polar_decoder_amd.montecarlo import seeded_conv
+    net = seeded_conv(256, 128, seed=0, device=dev)
     code = reference_polar_code(256, 128)
-    _, _, y = code.mc_generate(batch, 1.0, SEED, 0, 0, device=dev, want_msg=False)
-    net.logits(y)  # warm + weight packing
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        net.logits(y)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / iters
+    _, _, y = code.mc_generate(batch, 1.0, SEED, 0, rank * batch, device=dev, want_msg=False)
+    stream = torch.cuda.current_stream(dev)
+    t = timer(lambda: net.logits(y), iters=3, warm=1)
+    ms = event_ms(lambda: net.logits(y), 2, stream)
     flop_cw = 258.8e6  # SURVEY.md 8(d): 2 x (95.5 M conv + 33.9 M FC) MAC
     tf = flop_cw * batch / (ms / 1e3) / 1e12
-    return {"value": batch / (ms / 1e3), "unit": "codewords/s", "batch": batch, "avg_forward_ms": ms,
-            "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": tf, "peak_tflops_fp32": 157.3,
-            "frac": tf / 157.3, "config": "configs[4] per GPU: Polar(256,128) convNet embed 128"}
+    return {"value": world * batch / t, "unit": "codewords/s", "batch_per_gpu": batch, "avg_forward_ms": ms,
+            "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
+            "frac": tf / FP32_PEAK_TF, "config": "configs[4]: Polar(256,128) convNet embed 128, fp32"}
+
+
+# ------------------------------------------------------------------------------------ PMC traffic
+KERNEL_NAME = "sc_fast_kernel<64>"
 
 
 def traffic_child(args):
@@ -252,7 +444,6 @@ def pmc_traffic(args, timeout_s=240):
     import csv
     import glob
     import shutil
-    import subprocess
     import tempfile
     prof = shutil.which("rocprofv3")
     if prof is None:
@@ -280,11 +471,18 @@ def pmc_traffic(args, timeout_s=240):
     return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024, "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 read)"
 
 
+# ------------------------------------------------------------------------------------ main
 def main():
     args = parse()
     if args.traffic_child:
         return traffic_child(args)
-    world, rank, local = dist_setup(args)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return self_launch(args)
+    if int(env_world or 1) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks", file=sys.stderr)
+        return 2
+    world, rank, local = dist_setup()
     dev = torch.device("cuda", torch.cuda.current_device())
     from neural_polar_decoder_amd import reference_polar_code
 
@@ -294,8 +492,10 @@ def main():
     cw0 = rank * B  # weak scaling: every rank owns its own codeword range
     # the received words of every SNR point, back to back (n_snr, B, N), resident before timing
     yall = torch.empty(len(snrs), B, N_CODE, dtype=torch.float32, device=dev)
+    msg = None
     for si, snr in enumerate(snrs):
-        code.mc_generate(B, snr, SEED, si, cw0, want_msg=False, out=yall[si])
+        m, _, _ = code.mc_generate(B, snr, SEED, si, cw0, want_msg=msg is None, out=yall[si])
+        msg = m if msg is None else msg
     ys = [yall[si] for si in range(len(snrs))]
     hat = torch.empty(len(snrs), B, K_CODE, dtype=torch.float32, device=dev)
     counters = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
@@ -304,16 +504,16 @@ def main():
     def step(events=None):
         # one step = the whole SNR sweep of the batch, one launch (npd_sc_decode_mc_sweep)
         if events is not None:
-            events[0][0].record(stream)
+            events[0].record(stream)
         code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, counters, msg_hat=hat)
         if events is not None:
-            events[0][1].record(stream)
+            events[1].record(stream)
 
     for _ in range(args.warmup):
         step()
     counters.zero_()
     torch.cuda.synchronize()
-    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -324,8 +524,15 @@ def main():
     el = time.perf_counter() - t0
     el_t = allreduce(torch.tensor([el], dtype=torch.float64, device=dev), _max(), world)
     elapsed = float(el_t.item())
-    launch_ms = [e[0].elapsed_time(e[1]) for row in ev for e in row]
+    rank_ms = [el / args.steps * 1e3]
+    if world > 1:
+        import torch.distributed as dist
+        g = [None] * world
+        dist.all_gather_object(g, el / args.steps * 1e3)
+        rank_ms = g
+    launch_ms = [e[0].elapsed_time(e[1]) for e in ev]
     avg_launch_s = float(np.mean(launch_ms)) / 1e3
+    per_step_counts = (counters // args.steps).cpu()  # the same words every step: counts scale exactly
     allreduce(counters, _sum(), world)
 
     total_cw = world * args.steps * len(snrs) * B
@@ -337,12 +544,30 @@ def main():
     n_cw = args.steps * world * B
     ber = {s: float(cnt[i, 0]) / (n_cw * K_CODE) for i, s in enumerate(snrs)}
     bler = {s: float(cnt[i, 1]) / n_cw for i, s in enumerate(snrs)}
-    # the decoder sees the same words every step: counts scale exactly with the step count
     ber_match = all(abs(bler[s] - ANCHORS[s][1]) < 4 * np.sqrt(ANCHORS[s][1] * (1 - ANCHORS[s][1]) * (1e-5 + 1 / B))
                     for s in snrs if s in ANCHORS)
 
+    timer = Timer(world, dev)
+    legs = {}
+    if not args.no_mc and hasattr(code, "sc_mc_sweep_fused"):
+        ref = per_step_counts.clone()
+        if world > 1:
+            ref = allreduce(per_step_counts.to(dev), _sum(), world).cpu()
+        legs["montecarlo"] = mc_leg(code, snrs, B, cw0, world, timer, dev, ref)
+    if not args.no_gru:
+        legs["sc_plus_gru"] = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg)
+        legs["crisp_gru"] = gru_leg(code, dev, ys[2], B, world, timer)
+    if not (args.no_gru and args.no_pac):
+        legs.update(pac_legs(snrs, B, rank, world, timer, dev, not args.no_gru, not args.no_pac))
+    if not args.no_scl:
+        legs["scl"] = scl_leg(code, dev, ys[2], snrs[2], world, timer)
+    if not args.no_lse:
+        legs["sc_lse"] = lse_leg(code, dev, ys[2], snrs[2], world, timer)
+    if not args.no_conv:
+        legs["conv_model"] = conv_leg(dev, rank, world, timer)
+
     if rank != 0:
-        return
+        return 0
     out = {
         "metric": "codewords/sec Polar(64,32) SC + CRISP-GRU decode, 1/2/4/8 GPU; BER match",
         "value": value,
@@ -357,9 +582,12 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (Philox msg -> Plotkin encode -> AWGN), resident in HBM before timing",
         "config": {"workload": "configs[1]: Polar(N=64,K=32) min-sum SC decode + fused BER/BLER count, "
-                               "batch 2^20 per SNR per GPU, SNR sweep 0-4 dB",
+                               "batch 2^20 per SNR per GPU, SNR sweep 0-4 dB (the SC half of the metric; the "
+                               "SC + CRISP-GRU eval step is the sc_plus_gru leg)",
                    "code": "Polar(64,32) 'polar' rate profile", "batch_per_snr_per_gpu": B, "snr_db": snrs,
                    "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
+        "world_size_rccl": world,
+        "rank_ms_per_step": rank_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": KERNEL_NAME + " (npd_sc_decode_mc_sweep: all SNR points in one launch)",
@@ -368,33 +596,17 @@ def main():
         "bler": {str(s): bler[s] for s in snrs},
         "ber_match": bool(ber_match),
     }
-    if not args.no_gru:
-        out["crisp_gru"] = gru_measure(code, dev, ys[2], snrs[2])
-    if not args.no_scl:
-        out["scl"] = scl_measure(code, dev, ys[2], snrs[2])
-    if not args.no_lse:
-        out["sc_lse"] = lse_measure(code, dev, ys[2], snrs[2])
-    if not args.no_conv:
-        out["conv_model"] = conv_measure(dev)
+    out.update(legs)
     if not args.no_traffic and world == 1:
         traffic, how = pmc_traffic(args)
         out["roofline"]["traffic"] = traffic
         out["roofline"]["traffic_source"] = how
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         ys_host = [y[: 1 << 18].cpu().numpy() for y in ys]
         out["cpu_baseline"] = cpu_baseline(ys_host, snrs, code.info_positions, args.cpu_seconds)
     print(json.dumps(out), flush=True)
-
-
-def _max():
-    import torch.distributed as dist
-    return dist.ReduceOp.MAX
-
-
-def _sum():
-    import torch.distributed as dist
-    return dist.ReduceOp.SUM
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -162,6 +162,20 @@ int npd_list_prune_select(const float* neg_metrics, int n, int keep, uint32_t* m
 int npd_sc_decode_mc_sweep(const npd_code* code, int n_snr, const float* y, const float* llr_scale, float* msg_hat,
                            uint64_t seed, uint64_t cw_offset, int64_t B, unsigned long long* counters, void* stream);
 
+/*
+ * The Monte-Carlo step in one launch, y never stored: for each of the n_snr segments s and codeword
+ * cw_offset .. cw_offset+B-1, the message (Philox message stream of `seed`), its codeword and the
+ * received word (noise stream snr_index0 + s, sigma[s]) are generated in registers exactly as
+ * npd_mc_generate writes them, SC-decoded with llr_scale[s] and counted into counters (n_snr, 2)
+ * (and msg_hat (n_snr, B, K) if non-NULL).  Equal, count for count, to npd_mc_generate (snr_index =
+ * snr_index0 + s) followed by npd_sc_decode_mc_sweep.  sigma and llr_scale are HOST arrays.  Polar
+ * codes with 8 <= N <= 64 (NPD_ENOTSUP otherwise).  Replaces the generate/decode/count body of the
+ * reference's eval loops (run_models.py:318-337, rnn_all.py:842-856) for the SC decoder.
+ */
+int npd_sc_mc_sweep_fused(const npd_code* code, int n_snr, const float* sigma, const float* llr_scale,
+                          uint32_t snr_index0, uint64_t seed, uint64_t cw_offset, int64_t B, float* msg_hat,
+                          unsigned long long* counters, void* stream);
+
 /* ---------------------------------------------------------------------------------- counters */
 /*
  * counters[0] += #(round(ref) != round(hat)), counters[1] += #rows with any such element, over

@@ -37,6 +37,8 @@ SIGNATURES = [
     ("npd_sc_decode_mc", c_int, [c_void_p, c_void_p, c_float, c_void_p, c_u64, c_u64, c_i64, c_void_p, c_void_p]),
     ("npd_sc_decode_mc_sweep", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_u64, c_u64, c_i64, c_void_p,
                                        c_void_p]),
+    ("npd_sc_mc_sweep_fused", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_u32, c_u64, c_u64, c_i64, c_void_p,
+                                      c_void_p, c_void_p]),
     ("npd_sc_decode_lse", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p, c_i64, c_void_p]),
     ("npd_sc_decode_soft", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p, c_void_p, c_i64,
                                    c_void_p]),

@@ -93,16 +93,21 @@ __device__ __forceinline__ u32x4 philox_block(uint64_t seed, uint32_t stream, ui
 // uniform in (0, 1], exact in fp32
 __device__ __forceinline__ float u01(uint32_t x) { return (float)((x >> 8) + 1u) * 5.9604644775390625e-08f; }
 
-// two Box-Muller pairs -> 4 standard normals (precise libm-class functions, no fast-math)
+// two Box-Muller pairs -> 4 standard normals on the transcendental units: r = sqrt(-2 ln u1) with
+// v_log_f32 (log2) and v_sqrt_f32; (cos, sin)(2 pi u2) with v_cos_f32 / v_sin_f32, whose argument is in
+// revolutions (u2 itself, in (0, 1]).  ~10 instructions per pair instead of the ~150 of the libm
+// functions; the oracle evaluates the same formula with glibc log2f / sqrtf and double-precision
+// sin / cos (agreement ~1e-6, tests/test_sc_gpu.py).
 __device__ __forceinline__ void normals4(const u32x4& o, float z[4]) {
-    const float r0 = sqrtf(-2.0f * logf(u01(o.x)));
-    const float t0 = 6.2831853071795864769f * u01(o.y);
-    const float r1 = sqrtf(-2.0f * logf(u01(o.z)));
-    const float t1 = 6.2831853071795864769f * u01(o.w);
-    z[0] = r0 * cosf(t0);
-    z[1] = r0 * sinf(t0);
-    z[2] = r1 * cosf(t1);
-    z[3] = r1 * sinf(t1);
+    constexpr float kM2Ln2 = -1.38629436111989061883f;  // -2 ln 2
+    const float r0 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(o.x)));
+    const float t0 = u01(o.y);
+    const float r1 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(o.z)));
+    const float t1 = u01(o.w);
+    z[0] = r0 * __builtin_amdgcn_cosf(t0);
+    z[1] = r0 * __builtin_amdgcn_sinf(t0);
+    z[2] = r1 * __builtin_amdgcn_cosf(t1);
+    z[3] = r1 * __builtin_amdgcn_sinf(t1);
 }
 
 // ------------------------------------------------------------------------------------- misc device

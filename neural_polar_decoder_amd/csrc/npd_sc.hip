@@ -661,3 +661,22 @@ extern "C" int npd_sc_decode_mc_sweep(const npd_code* code, int n_snr, const flo
     }
     return NPD_OK;
 }
+
+namespace npd {
+int sc_fast_run_gen(const CodeParams& p, const float* sigma, const float* llr_scale, int n_seg, uint32_t snr_index0,
+                    float* msg, unsigned long long* counters, uint64_t seed, uint64_t cw_offset, int64_t B,
+                    hipStream_t s);
+}
+
+extern "C" int npd_sc_mc_sweep_fused(const npd_code* code, int n_snr, const float* sigma, const float* llr_scale,
+                                     uint32_t snr_index0, uint64_t seed, uint64_t cw_offset, int64_t B, float* msg_hat,
+                                     unsigned long long* counters, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_mc_sweep_fused: code is NULL");
+    NPD_ARG(n_snr >= 1 && n_snr <= 16, "npd_sc_mc_sweep_fused: 1 <= n_snr <= 16");
+    NPD_ARG(sigma != nullptr && llr_scale != nullptr, "npd_sc_mc_sweep_fused: sigma / llr_scale is NULL");
+    NPD_ARG(B >= 0, "npd_sc_mc_sweep_fused: B < 0");
+    NPD_ARG(counters != nullptr || msg_hat != nullptr, "npd_sc_mc_sweep_fused: no output");
+    if (B == 0) return NPD_OK;
+    return npd::sc_fast_run_gen(code->p, sigma, llr_scale, n_snr, snr_index0, msg_hat, counters, seed, cw_offset, B,
+                                (hipStream_t)stream);
+}

@@ -60,6 +60,8 @@ struct Args {
     int64_t B;
     int64_t ntiles;                  // tiles per segment
     float scale[kMaxSeg];
+    float sigma[kMaxSeg];            // GEN: channel sigma of each segment
+    uint32_t snr_index0;             // GEN: Philox noise stream of segment s = kStreamNoise + snr_index0 + s
     int n_seg;
     uint32_t count;
 };
@@ -407,10 +409,70 @@ __device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4
 #else
 #define STAMP(var) do { } while (0)
 #endif
+template <int N>
+__device__ __forceinline__ void frozen_words_init(Lane<N>& c, const CodeParams& p) {
+#pragma unroll
+    for (int w = 0; w < (N + 31) / 32; ++w) {
+        uint32_t fw = p.frozen[w];
+        asm volatile("" : "+s"(fw));
+        c.fz[w] = fw;
+    }
+}
+
 // decision-row stride: an odd number of dwords holding the K slot bytes (conflict-free dword reads)
 __host__ __device__ constexpr int row_stride(int K) { return 4 * ((((K > 0 ? K : 1) + 3) / 4) | 1); }
 
-template <int N, uint64_t MASK = 0, bool SPEC = false>
+// ---- GEN (fused Monte-Carlo): the received word of this lane's codeword is generated in registers,
+// value for value what npd_mc_generate writes (npd_gen.hip): message bits (Philox block 0 of the
+// message stream) scattered to the information positions, Plotkin butterfly as XOR on bit words, then
+// per 16-B chunk j the Philox noise block (cw, j) -> 4 Box-Muller normals -> y = x + fl32(sigma z).
+template <int N, uint64_t MASK, bool SPEC>
+__device__ __forceinline__ void codeword_bits(const uint32_t (&mw)[4], const uint32_t* fz, uint32_t (&U)[(N + 31) / 32]) {
+    constexpr int NW = (N + 31) / 32;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) U[w] = 0u;
+    int kk = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool frozen = SPEC ? (((MASK >> i) & 1ull) != 0) : (((fz[i >> 5] >> (i & 31)) & 1u) != 0);
+        if (!frozen) {
+            U[i >> 5] |= ((mw[kk >> 5] >> (kk & 31)) & 1u) << (i & 31);
+            ++kk;
+        }
+    }
+#pragma unroll
+    for (int h = 1; h < 32 && h < N; h <<= 1) {
+        uint32_t msk = 0;
+        for (int i = 0; i < 32; ++i)
+            if (((i / h) & 1) == 0) msk |= 1u << i;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) U[w] ^= (U[w] >> h) & msk;
+    }
+#pragma unroll
+    for (int hw = 1; hw < NW; hw <<= 1)
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if (((w / hw) & 1) == 0) U[w] ^= U[w + hw];
+}
+
+template <int N>
+__device__ __forceinline__ void gen_llrs(float* lv, const uint32_t (&U)[(N + 31) / 32], uint64_t seed, uint32_t stream,
+                                         uint64_t cw, float sigma, float scale) {
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) {
+        const u32x4 o = philox_block(seed, stream, cw, (uint32_t)j);
+        float z[4];
+        normals4(o, z);
+        const uint32_t bits = (U[(4 * j) >> 5] >> ((4 * j) & 31)) & 0xFu;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float xv = ((bits >> e) & 1u) ? -1.0f : 1.0f;
+            lv[4 * j + e] = rmul(scale, __fadd_rn(xv, __fmul_rn(sigma, z[e])));
+        }
+    }
+}
+
+template <int N, uint64_t MASK = 0, bool SPEC = false, bool GEN = false>
 __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) void sc_fast_kernel(const CodeParams p,
                                                                                                    const Args a) {
     constexpr int KC = N - __builtin_popcountll(MASK);  // information bits of a specialised code
@@ -451,7 +513,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
     int seg = (int)(g / (a.ntiles > 0 ? a.ntiles : 1));
     int64_t t = g - (int64_t)seg * a.ntiles;
     int cur_seg = seg;
-    if (NPD_SCF_PREFETCH && g < total)
+    if (!GEN && NPD_SCF_PREFETCH && g < total)
         load_tile<C>(nx, reinterpret_cast<const f4*>(a.y) + seg * segC, t, lane, a.B, segC - 1);
     unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0;
     unsigned long long ph[5] = {0, 0, 0, 0, 0};
@@ -488,7 +550,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
         // The seed is made opaque per tile so the key schedule is recomputed with scalar adds here
         // instead of being hoisted into 20 loop-invariant SGPRs (which spill to VGPR lanes).
         uint32_t mw[4] = {0u, 0u, 0u, 0u};
-        if (a.count && NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4) {
+        if ((GEN || a.count) && NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4) {
             uint64_t sd = a.seed;
             asm volatile("" : "+s"(sd));
             const u32x4 o = philox_block(sd, kStreamMsg, a.cw_offset + (uint64_t)(row0 + lane), 0u);
@@ -498,8 +560,18 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
             mw[3] = o.w;
         }
         STAMP(ts1);
+        if constexpr (GEN && !SPEC) frozen_words_init(c, p);
+        uint32_t Ubits[(N + 31) / 32];
+        if constexpr (GEN) {
+            codeword_bits<N, MASK, SPEC>(mw, c.fz, Ubits);
+            // previous tile's msg_hat before this tile's leaves overwrite the decision rows
+            if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg + pend_seg * a.B * K, pend_row0, pend_rows, K, lane, NB);
+            uint64_t sd = a.seed;
+            asm volatile("" : "+s"(sd));
+            gen_llrs<N>(c.lv + N, Ubits, sd, kStreamNoise + a.snr_index0 + (uint32_t)seg, a.cw_offset + (uint64_t)(row0 + lane),
+                        a.sigma[seg], scale);
+        } else {
         if (!NPD_SCF_PREFETCH) load_tile<C>(nx, y4, t, lane, a.B, last4);
-        {
         // ---- transpose the tile through LDS: chunk (lane + 64q) -> row r = (lane + 64q)/C, col chunk
 #pragma unroll
         for (int q = 0; q < C; ++q) {
@@ -529,7 +601,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
                 c.lv[N + 4 * q + 3] = rmul(scale, v.w);
             }
         }
-        }
+        }  // !GEN
         STAMP(ts3);
         // ---- decode.  The per-leaf frozen tests are loop-invariant; left alone the compiler hoists all
         // of them out of the tile loop and spills the resulting 64 SGPR pairs to VGPR lanes.  Making the
@@ -542,7 +614,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
                 c.fz[w] = fw;
             }
         };
-        if constexpr (!SPEC) frozen_words();
+        if constexpr (!SPEC && !GEN) frozen_words();
         {
             float inf = p.infty;
             asm volatile("" : "+s"(inf));
@@ -555,7 +627,13 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
             spec::snode<N, MASK, n, 0>(c, bad);
             if (__ballot(bad != 0u) != 0ull) {
                 // a shortcut's precondition failed on some lane (huge or zero LLRs): decode the tile again
-                // step by step from the LDS image of its received words
+                // step by step from the LDS image of its received words (GEN: regenerated)
+                if constexpr (GEN) {
+                    uint64_t sd = a.seed;
+                    asm volatile("" : "+s"(sd));
+                    gen_llrs<N>(c.lv + N, Ubits, sd, kStreamNoise + a.snr_index0 + (uint32_t)seg,
+                                a.cw_offset + (uint64_t)(row0 + lane), a.sigma[seg], scale);
+                } else {
 #pragma unroll
                 for (int q = 0; q < C; ++q) {
                     const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
@@ -563,6 +641,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
                     c.lv[N + 4 * q + 1] = rmul(scale, v.y);
                     c.lv[N + 4 * q + 2] = rmul(scale, v.z);
                     c.lv[N + 4 * q + 3] = rmul(scale, v.w);
+                }
                 }
                 c.slot = 0;
                 frozen_words();
@@ -634,7 +713,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
     }
 }
 
-template <int N, uint64_t MASK = 0, bool SPEC = false>
+template <int N, uint64_t MASK = 0, bool SPEC = false, bool GEN = false>
 static int launch(const CodeParams& p, Args a, hipStream_t s) {
     constexpr int KC = N - __builtin_popcountll(MASK);
     const int NB = row_stride(SPEC ? KC : p.K);
@@ -645,7 +724,7 @@ static int launch(const CodeParams& p, Args a, hipStream_t s) {
     while (wpb > 1 && (size_t)wpb * (per_wave + red) + N > 160 * 1024) --wpb;
     const size_t lds = (size_t)wpb * (per_wave + red) + N;
     a.ntiles = (a.B + kWave - 1) / kWave;
-    auto kern = sc_fast_kernel<N, MASK, SPEC>;
+    auto kern = sc_fast_kernel<N, MASK, SPEC, GEN>;
     static bool attr = false;
     if (!attr) {
         NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -678,6 +757,45 @@ static bool spec_disabled() {
 // eligible: Polar, 8 <= N <= 64, K <= 128 (one Philox block of message bits), y 16-B aligned
 bool sc_fast_eligible(const CodeParams& p, const void* y) {
     return !p.pac && p.N >= 8 && p.N <= 64 && p.K <= 128 && (((uintptr_t)y) & 15) == 0;
+}
+
+// fused Monte-Carlo sweep: same eligibility as the decode path minus the y pointer
+int sc_fast_run_gen(const CodeParams& p, const float* sigma, const float* llr_scale, int n_seg, uint32_t snr_index0,
+                    float* msg, unsigned long long* counters, uint64_t seed, uint64_t cw_offset, int64_t B,
+                    hipStream_t s) {
+    if (n_seg < 1 || n_seg > scf::kMaxSeg) return fail(NPD_EINVAL, "sc_mc_sweep_fused: 1 <= segments <= 16");
+    if (p.pac || p.N < 8 || p.N > 64 || p.K > 128)
+        return fail(NPD_ENOTSUP, "sc_mc_sweep_fused: Polar codes with 8 <= N <= 64 (use npd_mc_generate + "
+                                 "npd_sc_decode_mc otherwise)");
+    scf::Args a{};
+    a.y = nullptr;
+    a.msg = msg;
+    a.counters = counters;
+    a.seed = seed;
+    a.cw_offset = cw_offset;
+    a.B = B;
+    a.n_seg = n_seg;
+    a.snr_index0 = snr_index0;
+    for (int i = 0; i < n_seg; ++i) {
+        a.scale[i] = llr_scale[i];
+        a.sigma[i] = sigma[i];
+    }
+    a.count = counters ? 1u : 0u;
+    if (!spec_disabled()) {
+        uint64_t m = 0;
+        for (int i = 0; i < p.N; ++i)
+            if ((p.frozen[i >> 5] >> (i & 31)) & 1u) m |= 1ull << i;
+#define NPD_SPEC(NN, MM) \
+        if (p.N == NN && m == MM##ull) return scf::launch<NN, MM##ull, true, true>(p, a, s);
+        NPD_SPEC_CODES(NPD_SPEC)
+#undef NPD_SPEC
+    }
+    switch (p.N) {
+        case 8: return scf::launch<8, 0, false, true>(p, a, s);
+        case 16: return scf::launch<16, 0, false, true>(p, a, s);
+        case 32: return scf::launch<32, 0, false, true>(p, a, s);
+        default: return scf::launch<64, 0, false, true>(p, a, s);
+    }
 }
 
 int sc_fast_run(const CodeParams& p, const float* y, const float* llr_scale, int n_seg, float* msg,

@@ -105,17 +105,22 @@ class MonteCarlo:
 class SCMonteCarlo(MonteCarlo):
     """Polar / PAC SC decoding: fused generate (npd_mc_generate) + decode-and-count (npd_sc_decode_mc)."""
 
-    def __init__(self, code, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
+    def __init__(self, code, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None, fused=True):
         device = torch.device(device or "cuda")
         super().__init__(code.K, snrs, total_cw, batch, seed, rank, world, device)
         self.code = code
         self._y = None
+        # Polar N <= 64: generation fused into the decode kernel (npd_sc_mc_sweep_fused), y never stored
+        self.fused = bool(fused) and hasattr(code, "sc_mc_sweep_fused") and code.N <= 64 and len(self.snrs) <= 16
 
     def count_batch(self, si, snr, cw_offset, n, counters_row):
         _, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=False)
         self.code.sc_decode_mc(y, snr, self.seed, cw_offset, counters_row)
 
     def count_sweep(self, cw_offset, n, counters):
+        if self.fused:
+            self.code.sc_mc_sweep_fused(n, self.snrs, self.seed, cw_offset, counters)
+            return
         if not hasattr(self.code, "sc_decode_mc_sweep") or len(self.snrs) > 16:
             return super().count_sweep(cw_offset, n, counters)
         # Polar: every SNR point of the batch in one decode launch (npd_sc_decode_mc_sweep)
@@ -132,7 +137,7 @@ class SCLMonteCarlo(SCMonteCarlo):
     npd_scl_decode_mc (decode and count in one launch)."""
 
     def __init__(self, code, list_size, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
-        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device)
+        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device, fused=False)
         self.list_size = int(list_size)
 
     def count_batch(self, si, snr, cw_offset, n, counters_row):
@@ -149,7 +154,7 @@ class LSEMonteCarlo(SCMonteCarlo):
 
     def __init__(self, code, snrs, total_cw, batch, seed=1234, hard_decision=False, rank=None, world=None,
                  device=None):
-        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device)
+        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device, fused=False)
         self.hard_decision = bool(hard_decision)
 
     def count_batch(self, si, snr, cw_offset, n, counters_row):
@@ -161,25 +166,83 @@ class LSEMonteCarlo(SCMonteCarlo):
         return MonteCarlo.count_sweep(self, cw_offset, n, counters)
 
 
-class GRUMonteCarlo(MonteCarlo):
-    """CRISP GRU decoding (rnn_all.py:874-878): decoded[:, info] vs the message, counted on device."""
+class DecoderMonteCarlo(MonteCarlo):
+    """A neural decoder's Monte-Carlo: fused generation (npd_mc_generate, message kept), the decoder's
+    (n, N) decisions, and decisions[:, info] counted against the message on the device
+    (errors_ber / errors_bler semantics, utils.py:17-51).  Subclasses provide ``decisions(y)``."""
 
-    def __init__(self, code, net, decoder, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
+    def __init__(self, code, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
         device = torch.device(device or "cuda")
         super().__init__(code.K, snrs, total_cw, batch, seed, rank, world, device)
-        self.code, self.net, self.decoder = code, net, decoder
+        self.code = code
         info = getattr(code, "info_positions", None)
-        self.info = torch.as_tensor(np.asarray(info if info is not None else code.B), device=device)
+        self.info_np = np.asarray(info if info is not None else code.B, dtype=np.int64)
+        self.info = torch.as_tensor(self.info_np, device=device)
+
+    def generate(self, si, snr, cw_offset, n):
+        msg, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=True)
+        return msg, y
+
+    def decisions(self, y):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def count(self, msg, hat, counters_row):
+        from .utils import count_errors
+        count_errors(msg, hat, counters_row)
 
     def count_batch(self, si, snr, cw_offset, n, counters_row):
-        from .utils import count_errors
-        msg, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=True)
-        dec = self.decoder.decode(self.net, False, y)
-        count_errors(msg, dec.index_select(1, self.info), counters_row)
+        msg, y = self.generate(si, snr, cw_offset, n)
+        self.count(msg, self.decisions(y).index_select(1, self.info), counters_row)
+
+
+class GRUMonteCarlo(DecoderMonteCarlo):
+    """CRISP GRU decoding (rnn_all.py:874-878 Polar; rnn_all.py:679-700 PAC): decoded[:, info] vs the
+    message."""
+
+    def __init__(self, code, net, decoder, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
+        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device)
+        self.net, self.decoder = net, decoder
+
+    def decisions(self, y):
+        return self.decoder.decode(self.net, False, y)
+
+
+class ConvMonteCarlo(DecoderMonteCarlo):
+    """convNet decoding (run_models.py:333-337, testXformer): sign of the LayerNorm output at the info
+    positions vs the message."""
+
+    def __init__(self, code, net, snrs, total_cw, batch, seed=1234, rank=None, world=None, device=None):
+        super().__init__(code, snrs, total_cw, batch, seed, rank, world, device)
+        self.net = net
+
+    def decisions(self, y):
+        return self.net.logits(y)[1]
+
+
+def seeded_crisp(code, feature_size=64, depth=2, seed=0, device="cuda", onehot=True, precision="fp32"):
+    """(net, RNN_decoder) with PyTorch-default-initialised weights under torch.manual_seed(seed): the
+    reference ships no trained checkpoint (rnn_all.py:294-398 architecture, y_input + onehot)."""
+    from .rnn import RNN_Model, RNN_decoder
+    N = code.N
+    torch.manual_seed(seed)
+    net = RNN_Model("GRU", N + 1 + int(onehot), feature_size, 1, depth, N, 0, 0).to(device).eval()
+    info = getattr(code, "info_positions", None)
+    dec = RNN_decoder("y_input", N, np.asarray(info if info is not None else code.B), onehot=onehot,
+                      precision=precision)
+    return net, dec
+
+
+def seeded_conv(N, embed_dim=128, seed=0, device="cuda"):
+    """convNet (models.py:691-772) with PyTorch-default-initialised weights under torch.manual_seed(seed)."""
+    from .models import convNet
+    torch.manual_seed(seed)
+    cfg = argparse.Namespace(embed_dim=embed_dim, max_len=N, N=N, dont_use_bias=False, dropout=0.0)
+    return convNet(cfg).to(device).eval()
 
 
 def _main(argv=None):
-    ap = argparse.ArgumentParser(description="MI355X BER/BLER Monte-Carlo (SC decoding)")
+    ap = argparse.ArgumentParser(description="MI355X BER/BLER Monte-Carlo (SC, SC-List, exact-LSE SC, CRISP GRU, "
+                                             "convNet decoders)")
     ap.add_argument("--code", choices=["polar", "pac"], default="polar")
     ap.add_argument("--N", type=int, default=64)
     ap.add_argument("--K", type=int, default=32)
@@ -195,6 +258,14 @@ def _main(argv=None):
     ap.add_argument("--list_size", type=int, default=None, help="also run SC-List with this list size (Polar)")
     ap.add_argument("--lse", action="store_true", help="also run the exact-LSE sc_decode (Polar, polar.py:209)")
     ap.add_argument("--hard_decision", action="store_true", help="exact-LSE SC with sign decisions (else tanh)")
+    ap.add_argument("--crisp", action="store_true", help="also run the CRISP GRU decoder (rnn_all.py:874)")
+    ap.add_argument("--crisp_checkpoint", default=None, help="rnn_all.py checkpoint ({'net', 'args'}) for --crisp")
+    ap.add_argument("--rnn_feature_size", type=int, default=64, help="--crisp without checkpoint: hidden size")
+    ap.add_argument("--rnn_depth", type=int, default=2, help="--crisp without checkpoint: GRU layers")
+    ap.add_argument("--conv", action="store_true", help="also run the convNet decoder (run_models.py:333)")
+    ap.add_argument("--conv_checkpoint", default=None, help="run_models.py checkpoint ({'xformer', 'args'}) for --conv")
+    ap.add_argument("--embed_dim", type=int, default=128, help="--conv without checkpoint: channels")
+    ap.add_argument("--init_seed", type=int, default=0, help="torch seed of the untrained (seeded) decoder weights")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
@@ -223,8 +294,30 @@ def _main(argv=None):
         if a.code != "polar":
             raise SystemExit("--lse: the exact-LSE sc_decode is defined for Polar codes only (polar.py:209)")
         lse = LSEMonteCarlo(code, snrs, a.test_size, a.batch_size, a.seed, hard_decision=a.hard_decision).run()
+    crisp = None
+    if a.crisp:
+        if a.crisp_checkpoint:
+            from .datasets import rnn_from_checkpoint
+            net, dec, ccode = rnn_from_checkpoint(a.crisp_checkpoint)
+            if ccode.N != a.N or ccode.K != a.K:
+                raise SystemExit("--crisp_checkpoint was trained for a different (N, K)")
+        else:
+            net, dec = seeded_crisp(code, a.rnn_feature_size, a.rnn_depth, a.init_seed)
+        crisp = GRUMonteCarlo(code, net, dec, snrs, a.test_size, a.batch_size, a.seed).run()
+    conv = None
+    if a.conv:
+        if a.conv_checkpoint:
+            from .datasets import convnet_from_checkpoint
+            cnet = convnet_from_checkpoint(a.conv_checkpoint)
+        else:
+            cnet = seeded_conv(a.N, a.embed_dim, a.init_seed)
+        conv = ConvMonteCarlo(code, cnet, snrs, a.test_size, a.batch_size, a.seed).run()
     if _dist() is None or _dist().get_rank() == 0:
         print("Test SNRs : ", snrs)
+        if crisp is not None:
+            print("BERs of RNN: {0}".format(crisp.ber))
+        if conv is not None:
+            print("BERs of Xformer: {0}".format(conv.ber))
         print("BERs of SC decoding: {0}".format(res.ber))
         print("BLERs of SC decoding: {0}".format(res.bler))
         rec = {"sc": res.as_dict()}
@@ -236,6 +329,12 @@ def _main(argv=None):
             print("BERs of exact-LSE SC decoding: {0}".format(lse.ber))
             print("BLERs of exact-LSE SC decoding: {0}".format(lse.bler))
             rec["sc_lse"] = dict(lse.as_dict(), hard_decision=a.hard_decision)
+        if crisp is not None:
+            print("BLERs of RNN: {0}".format(crisp.bler))
+            rec["crisp_gru"] = crisp.as_dict()
+        if conv is not None:
+            print("BLERs of Xformer: {0}".format(conv.bler))
+            rec["conv"] = conv.as_dict()
         print(json.dumps(rec))
     return res
 

@@ -272,6 +272,19 @@ class PolarCode:
                    "npd_sc_decode_mc_sweep")
         return counters
 
+    def sc_mc_sweep_fused(self, B, snrs, seed, cw_offset, counters, msg_hat=None, snr_index0=0):
+        """counters (n_snr, 2) += errors of SC on B fresh codewords per SNR, generated in the decode kernel
+        (npd_sc_mc_sweep_fused): identical counts to mc_generate(snr_index = snr_index0 + s) followed by
+        sc_decode_mc_sweep.  Polar codes, N <= 64."""
+        _lib.require_gpu(counters, "counters")
+        sig = np.asarray([sigma_f32(s) for s in snrs], dtype=np.float32)
+        scl = np.asarray([llr_scale(s) for s in snrs], dtype=np.float32)
+        _lib.check(_lib.load().npd_sc_mc_sweep_fused(self.code.h, len(sig), sig.ctypes.data_as(ctypes.c_void_p),
+                                                     scl.ctypes.data_as(ctypes.c_void_p), int(snr_index0), int(seed),
+                                                     int(cw_offset), int(B), _lib.ptr(msg_hat), _lib.ptr(counters),
+                                                     _lib.stream_of(counters.device)), "npd_sc_mc_sweep_fused")
+        return counters
+
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
         _lib.check(_lib.load().npd_sc_decode_mc(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(msg_hat), int(seed),

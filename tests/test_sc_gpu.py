@@ -311,3 +311,51 @@ def test_sweep_equals_per_snr_calls(N, K, B):
         code.sc_decode_mc(y[i], s, 11, 7, c2[i], msg_hat=h)
         assert torch.equal(h, h1[i]), s
     assert torch.equal(c1, c2)
+
+
+@pytest.mark.parametrize("N,K,B", [(64, 32, 100_003), (32, 16, 5000), (16, 8, 777), (64, 22, 3001), (8, 4, 4099)])
+def test_fused_mc_sweep_equals_generate_then_decode(N, K, B):
+    """npd_sc_mc_sweep_fused (message -> codeword -> AWGN generated inside the decode kernel, y never
+    stored) == npd_mc_generate + npd_sc_decode_mc_sweep: identical msg_hat and counters at every SNR,
+    including 25 dB, where the specialised decoder's closed-form subtrees fall back to step-by-step SC
+    (regenerated received words)."""
+    from neural_polar_decoder_amd import PolarCode, reference_polar_code
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    if K == 22:
+        info = polar_info_positions(N, K)
+        code = PolarCode(int(np.log2(N)), K, F=np.setdiff1d(np.arange(N), info))
+    else:
+        code = reference_polar_code(N, K)
+    snrs = [-1.0, 1.5, 3.0, 25.0]
+    seed, off, si0 = 13, 12345, 2
+    y = torch.empty(len(snrs), B, N, device=DEV)
+    for i, s in enumerate(snrs):
+        code.mc_generate(B, s, seed, si0 + i, off, out=y[i], want_msg=False)
+    c1 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    h1 = torch.empty(len(snrs), B, K, device=DEV)
+    code.sc_decode_mc_sweep(y, snrs, seed, off, c1, msg_hat=h1)
+    c2 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    h2 = torch.empty(len(snrs), B, K, device=DEV)
+    code.sc_mc_sweep_fused(B, snrs, seed, off, c2, msg_hat=h2, snr_index0=si0)
+    assert torch.equal(h1, h2)
+    assert torch.equal(c1, c2), (c1.tolist(), c2.tolist())
+
+
+def test_fused_mc_rejects_unsupported_codes():
+    import argparse
+    from neural_polar_decoder_amd import PAC, NpdError, reference_polar_code
+    c = torch.zeros(1, 2, dtype=torch.int64, device=DEV)
+    with pytest.raises(NpdError):
+        reference_polar_code(128, 64).sc_mc_sweep_fused(64, [1.0], 1, 0, c)
+    pac = PAC(argparse.Namespace(target_K=64), 128, 64, 91)
+    assert not hasattr(pac, "sc_mc_sweep_fused")
+
+
+def test_montecarlo_fused_equals_unfused():
+    """SCMonteCarlo with the fused sweep == the generate-then-decode path, counter for counter."""
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import SCMonteCarlo
+    code = reference_polar_code(64, 32)
+    a = SCMonteCarlo(code, [0.0, 2.0, 4.0], 70_001, 30_000, seed=3).run()
+    b = SCMonteCarlo(code, [0.0, 2.0, 4.0], 70_001, 30_000, seed=3, fused=False).run()
+    assert a.bit_errors == b.bit_errors and a.block_errors == b.block_errors
