@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--no-mc", action="store_true", help="skip the fused Monte-Carlo leg")
     ap.add_argument("--no-pac", action="store_true", help="skip the PAC(128,64) SC leg")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # CPU test of the launcher
     return ap.parse_args()
 
 
@@ -482,6 +483,9 @@ def main():
     if int(env_world or 1) != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks", file=sys.stderr)
         return 2
+    if args.launch_probe:  # launcher check without a GPU: report the rank layout and stop
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(env_world or 1)}), flush=True)
+        return 0
     world, rank, local = dist_setup()
     dev = torch.device("cuda", torch.cuda.current_device())
     from neural_polar_decoder_amd import reference_polar_code
