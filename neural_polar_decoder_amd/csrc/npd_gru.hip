@@ -666,6 +666,219 @@ static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
     return launch_check("gru_decode_bf_kernel launch");
 }
 
+// =============================================================================== wide hidden sizes
+// F = 128 / 256 / 512 (the CRISP curriculum trains F = 512, 2 layers: run_crisp.sh).  The weights
+// (3 x 3F x F fp32 = 9.4 MB at F = 512) no longer fit in LDS, so the per-step matvecs of a 32-codeword
+// tile become weight-streaming GEMMs: one workgroup of NW = min(8, F/32) waves owns 32 codewords, each
+// wave owns HPW = F/32/NW hidden tiles (its r, z, n gate rows), the A operands stream from L2 / MALL in
+// the same permuted image as the narrow kernel (prefetched one 4-k-step group ahead), and the hidden
+// states of both layers live in LDS in B-operand order (k-step s, lane half, codeword): a wave writes
+// its updated tiles with 16-B stores and every wave reads the whole state with ds_read_b128.  The y
+// projection W_ih0[:, :N] y is recomputed every step from an LDS copy of the tile's received words
+// (+ N/2 k-steps per 3F x F matvec: < 5 % of the step's MFMAs) instead of holding 3F x 32 values in
+// registers.  Barriers separate each layer's GEMM (reads the old state) from its update (overwrites
+// it); the output Linear(F, 1) is reduced across waves through LDS in a fixed order.
+template <int F>
+struct WideGeo {
+    static constexpr int HT = F / 32;
+    static constexpr int NW = HT < 8 ? HT : 8;
+    static constexpr int HPW = HT / NW;
+};
+
+int wide_lds_bytes(int N, int F, int L) {
+    const int nw = (F / 32) < 8 ? F / 32 : 8;
+    return (L * F * 32 + N * 32 + nw * 32) * 4;
+}
+
+// acc[D0|D1|D2][j] += W[tiles k*HT + jt0 + j, k = 0, 1, 2] . B over kg groups of 4 k-steps.
+// W: f4 image of one matrix ([tile][group][lane]), B: LDS state in B-operand order ([group][lane]).
+template <int HPW, int D0, int D1, int D2>
+__device__ __forceinline__ void wide_chain(const f4* __restrict__ W, int kg, int HT, int jt0,
+                                           const f4* __restrict__ Bs, int lane, f16v (&acc)[4][HPW]) {
+    constexpr int D[3] = {D0, D1, D2};
+    f4 wc[3][HPW];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int j = 0; j < HPW; ++j) wc[k][j] = W[((size_t)(k * HT + jt0 + j) * kg + 0) * 64 + lane];
+    for (int q = 0; q < kg; ++q) {
+        f4 wn[3][HPW];
+        if (q + 1 < kg) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) wn[k][j] = W[((size_t)(k * HT + jt0 + j) * kg + q + 1) * 64 + lane];
+        }
+        const f4 b = Bs[q * 64 + lane];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) acc[D[k]][j] = mfma(wc[k][j][e], b[e], acc[D[k]][j]);
+        if (q + 1 < kg) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) wc[k][j] = wn[k][j];
+        }
+    }
+}
+
+// one hidden tile's GRU update against its old value in the LDS state (B-operand order)
+template <int HPW>
+__device__ __forceinline__ void wide_update(f4* __restrict__ Hs, int jt, int lane, f16v& hv, const f16v& ar,
+                                            const f16v& az, const f16v& ain, const f16v& ahn) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const f4 v = Hs[(4 * jt + q) * 64 + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[4 * q + e] = v[e];
+    }
+    gru_update(hv, ar, az, ain, ahn);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        f4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = hv[4 * q + e];
+        Hs[(4 * jt + q) * 64 + lane] = v;
+    }
+}
+
+template <int F, int L>
+__global__ __launch_bounds__(64 * WideGeo<F>::NW) void gru_wide_kernel(const Args a) {
+    using G = Geo<F, L>;
+    using WG = WideGeo<F>;
+    constexpr int TT = G::TT, HT = G::HT, KG = G::KG, NW = WG::NW, HPW = WG::HPW;
+    extern __shared__ __attribute__((aligned(16))) f4 lds4[];
+    const int N = a.N;
+    f4* const Hs0 = lds4;
+    f4* const Hs1 = lds4 + (L == 2 ? F * 8 : 0);
+    f4* const Ys = lds4 + L * F * 8;
+    float* const part = reinterpret_cast<float*>(Ys + N * 8);
+    const float* img = a.img;
+    const f4* W0 = reinterpret_cast<const f4*>(img);
+    const f4* W1 = reinterpret_cast<const f4*>(img + (size_t)G::G_SIZE);
+    const f4* W2 = reinterpret_cast<const f4*>(img + 2 * (size_t)G::G_SIZE);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int half = lane >> 5;
+    const int col = lane & 31;
+    const int jt0 = wave * HPW;
+    const int ng = N / 8;
+    const int64_t ntiles = (a.B + 31) / 32;
+    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float one_or_zero = half ? 0.0f : 1.0f;
+    constexpr int R = 0, Z = 1, IN = 2, HN = 3;
+
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t cw = tile * 32 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        __syncthreads();  // the previous tile's last readers are done
+        {
+            const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
+            for (int q = wave; q < ng; q += NW) Ys[q * 64 + lane] = yr[q];
+            for (int i = threadIdx.x; i < L * F * 8; i += NW * 64) lds4[i] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+        __syncthreads();
+        float xb = 1.0f;
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            const float xbe = half ? xb : 1.0f;
+            f16v acc[4][HPW];
+            f16v top[HPW];
+            // ================= layer 0: P = W_ih0[:, :N] y (r, z, in), then W_hh0 h0 (r, z, hn), then consts
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) acc[k][j] = zero;
+            wide_chain<HPW, R, Z, IN>(a.wy, ng, HT, jt0, Ys, lane, acc);
+            wide_chain<HPW, R, Z, HN>(W0, KG, HT, jt0, Hs0, lane, acc);
+#pragma unroll
+            for (int j = 0; j < HPW; ++j) {
+                const int jt = jt0 + j;
+                acc[R][j] = mfma(img[G::OFF_X + (0 * TT + jt) * 64 + lane], xbe, acc[R][j]);
+                acc[Z][j] = mfma(img[G::OFF_X + (0 * TT + HT + jt) * 64 + lane], xbe, acc[Z][j]);
+                acc[HN][j] = mfma(img[G::OFF_X + (0 * TT + 2 * HT + jt) * 64 + lane], xbe, acc[HN][j]);
+                acc[IN][j] = mfma(img[G::OFF_IN + jt * 64 + lane], xbe, acc[IN][j]);
+            }
+            __syncthreads();  // every wave has read h0
+#pragma unroll
+            for (int j = 0; j < HPW; ++j) wide_update<HPW>(Hs0, jt0 + j, lane, top[j], acc[R][j], acc[Z][j], acc[IN][j], acc[HN][j]);
+            __syncthreads();  // h0' complete
+            if constexpr (L == 2) {
+                // ================= layer 1: W_ih1 h0' (r, z, in) + consts, W_hh1 h1 (r, z, hn) + b_hn
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int j = 0; j < HPW; ++j) acc[k][j] = zero;
+                wide_chain<HPW, R, Z, IN>(W1, KG, HT, jt0, Hs0, lane, acc);
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) {
+                    const int jt = jt0 + j;
+                    acc[R][j] = mfma(img[G::OFF_X + (TT + jt) * 64 + lane], one_or_zero, acc[R][j]);
+                    acc[Z][j] = mfma(img[G::OFF_X + (TT + HT + jt) * 64 + lane], one_or_zero, acc[Z][j]);
+                    acc[IN][j] = mfma(img[G::OFF_X + (TT + 2 * HT + jt) * 64 + lane], one_or_zero, acc[IN][j]);
+                }
+                wide_chain<HPW, R, Z, HN>(W2, KG, HT, jt0, Hs1, lane, acc);
+#pragma unroll
+                for (int j = 0; j < HPW; ++j)
+                    acc[HN][j] = mfma(img[G::OFF_X + (2 * TT + 2 * HT + jt0 + j) * 64 + lane], one_or_zero, acc[HN][j]);
+                __syncthreads();  // every wave has read h1
+#pragma unroll
+                for (int j = 0; j < HPW; ++j)
+                    wide_update<HPW>(Hs1, jt0 + j, lane, top[j], acc[R][j], acc[Z][j], acc[IN][j], acc[HN][j]);
+            }
+            // ================= output: Linear(F, 1) on the top layer, reduced over the waves in a fixed order
+            float p = 0.0f;
+#pragma unroll
+            for (int j = 0; j < HPW; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) p += img[G::OFF_WL + (half * HT + jt0 + j) * 16 + i] * top[j][i];
+            p += __shfl_xor(p, 32, 64);
+            if (half == 0) part[wave * 32 + col] = p;
+            __syncthreads();
+            float out = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) out += part[w * 32 + col];
+            out += a.b_lin;
+            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+            float d;
+            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+            if (wave == 0 && half == 0 && valid) {
+                a.decoded[cw * N + jj] = d;
+                if (a.logits) a.logits[cw * N + ii] = out;
+            }
+            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+        }
+    }
+}
+
+template <int F, int L>
+static int launch_wide(const Args& a, int N, hipStream_t s) {
+    using WG = WideGeo<F>;
+    auto kern = gru_wide_kernel<F, L>;
+    const size_t lds = (size_t)wide_lds_bytes(N, F, L);
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * WG::NW, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    const int64_t tiles = (a.B + 31) / 32;
+    const int grid = grid_for(tiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WG::NW), lds, s, a);
+    return launch_check("gru_wide_kernel launch");
+}
+
 }  // namespace gru
 }  // namespace npd
 
@@ -677,7 +890,11 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     *out = nullptr;
     NPD_ARG(weights != nullptr, "npd_gru_create: weights is NULL");
     NPD_ARG(N >= 8 && N <= kMaxN && N % 8 == 0, "npd_gru_create: N must be a multiple of 8 in [8, 256]");
-    NPD_ARG(F == 32 || F == 64, "npd_gru_create: hidden size F must be 32 or 64 in this build");
+    NPD_ARG(F == 32 || F == 64 || F == 128 || F == 256 || F == 512,
+            "npd_gru_create: hidden size F must be 32, 64, 128, 256 or 512");
+    NPD_ARG(F <= 64 || precision == 0, "npd_gru_create: the bf16 kernels cover F <= 64; F > 64 runs fp32");
+    NPD_ARG(F <= 64 || gru::wide_lds_bytes(N, F, layers) <= 160 * 1024,
+            "npd_gru_create: F = 512 with 2 layers needs N <= 128 (LDS holds both states and the tile's y)");
     NPD_ARG(layers == 1 || layers == 2, "npd_gru_create: 1 or 2 GRU layers supported");
     NPD_ARG(precision >= 0 && precision <= 2, "npd_gru_create: precision must be 0 (fp32), 1 (bf16x3) or 2 (bf16)");
     NPD_ARG(precision == 0 || N % 16 == 0, "npd_gru_create: bf16 paths need N % 16 == 0");
@@ -695,7 +912,13 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
         else if (precision == 1) gru::build_image_bf<FF, LL, 3>(weights, N, onehot, img, wy, b_lin, wy_lo); \
         else gru::build_image_bf<FF, LL, 1>(weights, N, onehot, img, wy, b_lin, wy_lo);               \
     } while (0)
-    if (F == 64 && layers == 2) NPD_BUILD(64, 2);
+    if (F == 512 && layers == 2) gru::build_image<512, 2>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 512) gru::build_image<512, 1>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 256 && layers == 2) gru::build_image<256, 2>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 256) gru::build_image<256, 1>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 128 && layers == 2) gru::build_image<128, 2>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 128) gru::build_image<128, 1>(weights, N, onehot, img, wy, b_lin);
+    else if (F == 64 && layers == 2) NPD_BUILD(64, 2);
     else if (F == 64) NPD_BUILD(64, 1);
     else if (layers == 2) NPD_BUILD(32, 2);
     else NPD_BUILD(32, 1);
@@ -766,6 +989,11 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
         if (g->layers == 2) NPD_LBF(32, 2);
         NPD_LBF(32, 1);
 #undef NPD_LBF
+    }
+    if (g->F > 64) {
+        if (g->F == 512) return g->layers == 2 ? gru::launch_wide<512, 2>(a, g->N, s) : gru::launch_wide<512, 1>(a, g->N, s);
+        if (g->F == 256) return g->layers == 2 ? gru::launch_wide<256, 2>(a, g->N, s) : gru::launch_wide<256, 1>(a, g->N, s);
+        return g->layers == 2 ? gru::launch_wide<128, 2>(a, g->N, s) : gru::launch_wide<128, 1>(a, g->N, s);
     }
     if (g->F == 64 && g->layers == 2) return gru::launch<64, 2>(g, a, s);
     if (g->F == 64) return gru::launch<64, 1>(g, a, s);

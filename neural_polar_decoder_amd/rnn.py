@@ -62,7 +62,7 @@ class RNN_Model(nn.Module):
     def fused_supported(self) -> bool:
         return (self.rnn_type == "GRU" and self.output_size == 1 and self.y_depth == 0 and self.out_linear_depth == 1
                 and not self.bidirectional and isinstance(self.layernorm, nn.Identity)
-                and self.feature_size in (32, 64) and self.num_rnn_layers in (1, 2))
+                and self.feature_size in (32, 64, 128, 256, 512) and self.num_rnn_layers in (1, 2))
 
 
 def pack_gru_weights(net: nn.Module, layers: int) -> np.ndarray:

@@ -36,6 +36,31 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name))
 
 
+def weights_digest(sd):
+    """sha256 over a state dict's arrays in sorted key order (tests/golden/gen_golden.py)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k], np.float32).tobytes())
+    return h.hexdigest()
+
+
+def gru_state_dict(d):
+    """A GRU fixture's weights: stored arrays, or (F > 64) regenerated from the stored torch seed with this
+    package's RNN_Model (same parameter draws as the reference's) and checked against the stored digest."""
+    if "w_seed" not in d.files:
+        return {k[2:]: np.asarray(d[k]) for k in d.files if k.startswith("w.")}
+    import torch
+    from neural_polar_decoder_amd.rnn import RNN_Model
+    N, F = int(d["N"]), int(d["F"])
+    torch.manual_seed(int(d["w_seed"]))
+    net = RNN_Model("GRU", N + 1 + int(d["onehot"]), F, 1, 2, N, 0, 0, "selu", 0.0, False, out_linear_depth=1)
+    sd = {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}
+    assert weights_digest(sd) == bytes(d["w_digest"]).decode(), "regenerated GRU weights differ from the fixture's"
+    return sd
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import oracle as O

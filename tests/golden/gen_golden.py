@@ -190,6 +190,12 @@ def gen_scl_long():
     gen_scl([(128, 64, 4, 16), (256, 128, 4, 8), (128, 64, 8, 8)], seed=9)
 
 
+def gen_gru_wide():
+    """Hidden sizes above 64: the CRISP curriculum's F = 512, 2 layers (run_crisp.sh), and F = 128."""
+    gen_gru([("gru_crisp_64_22_f512", "rev_polar", 64, 22, 512, True, False, 160),
+             ("gru_polar_32_16_f128_noonehot", "Polar", 32, 16, 128, False, False, 200)])
+
+
 def gen_lse():
     """PolarCode.sc_decode (exact-LSE SC, polar.py:209-279) with args.hard_decision True and False:
     msg_hat and decoded_bits (decode(llrs, 0, 0, zeros) -- the call sc_decode makes, polar.py:221)."""
@@ -296,14 +302,28 @@ def gen_errors():
 
 
 # -------------------------------------------------------------------------------------------- GRU
-def gen_gru():
-    cases = [("gru_polar_64_32", "Polar", 64, 32, 64, True, False, 512),
-             ("gru_pac_128_64", "PAC", 128, 64, 64, True, False, 128),
-             ("gru_polar_16_8_noonehot_rev", "Polar", 16, 8, 32, False, True, 256)]
+def weights_digest(sd):
+    """sha256 over the state dict's arrays in sorted key order (fp32 bytes)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k], np.float32).tobytes())
+    return h.hexdigest()
+
+
+def gen_gru(cases=None):
+    cases = cases or [("gru_polar_64_32", "Polar", 64, 32, 64, True, False, 512),
+                      ("gru_pac_128_64", "PAC", 128, 64, 64, True, False, 128),
+                      ("gru_polar_16_8_noonehot_rev", "Polar", 16, 8, 32, False, True, 256)]
     for name, ctype, N, K, F, onehot, rev, B in cases:
-        torch.manual_seed(2024 + N)
+        torch.manual_seed(2024 + N + (F if F > 64 else 0))  # == the seed stored for F > 64
         if ctype == "Polar":
             code = polar_code(N, K)
+            info = np.asarray(code.info_positions, np.int64)
+        elif ctype == "rev_polar":  # run_crisp.sh: --rate_profile rev_polar --target_K 22
+            rnn_m.args = ns(target_K=22, K=K, N=N)
+            code = rnn_m.get_code("Polar", "rev_polar", N, K)
             info = np.asarray(code.info_positions, np.int64)
         else:
             code = pac_m.PAC(ns(target_K=K), N, K, 91)
@@ -317,7 +337,7 @@ def gen_gru():
         h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
         for snr in SNRS:
             msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
-            x = code.encode_plotkin(msg) if ctype == "Polar" else code.pac_encode(msg, scheme="RM")
+            x = code.pac_encode(msg, scheme="RM") if ctype == "PAC" else code.encode_plotkin(msg)
             y = code.channel(x, float(snr))
             rec.clear()
             d = dec.decode(net, False, y)
@@ -325,9 +345,23 @@ def gen_gru():
             logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
         h.remove()
         sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        extra = {"w." + k: v for k, v in sd.items()}
+        if F > 64:
+            # 9.4 MB of weights at F = 512: store the torch seed that regenerates them (this package's RNN_Model
+            # draws the identical parameters, checked here) and a digest the tests verify before use
+            sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+            from neural_polar_decoder_amd.rnn import RNN_Model as OurModel
+            seed = 2024 + N + F
+            torch.manual_seed(seed)
+            ours = OurModel("GRU", N + 1 + int(onehot), F, 1, 2, N, 0, 0, "selu", 0.0, False, out_linear_depth=1)
+            torch.manual_seed(seed)
+            theirs = rnn_m.RNN_Model("GRU", N + 1 + int(onehot), F, 1, 2, N, 0, 0, "selu", 0.0, False,
+                                     out_linear_depth=1)
+            for k, v in theirs.state_dict().items():
+                assert torch.equal(v, ours.state_dict()[k]) and torch.equal(v, net.state_dict()[k]), k
+            extra = {"w_seed": np.int64(seed), "w_digest": np.bytes_(weights_digest(sd))}
         save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
-             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, onehot=int(onehot), rev=int(rev),
-             **{"w." + k: v for k, v in sd.items()})
+             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, onehot=int(onehot), rev=int(rev), **extra)
 
 
 # ------------------------------------------------------------------------------------------- conv
@@ -373,6 +407,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "pac", "errors", "gru", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "pac", "errors", "gru", "gru_wide", "conv"]
     for w in which:
         globals()["gen_" + w]()

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import golden, gru_state_dict
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -21,13 +21,13 @@ def build(d, precision="fp32"):
     N, F = int(d["N"]), int(d["F"])
     onehot = bool(d["onehot"])
     net = RNN_Model("GRU", N + 1 + int(onehot), F, 1, 2, N, 0, 0, "selu", 0.0, False, out_linear_depth=1).to(DEV)
-    sd = {k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w.")}
-    net.load_state_dict(sd)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in gru_state_dict(d).items()})
     dec = RNN_decoder("y_input", N, d["info"], onehot=onehot, reverse_order=bool(d["rev"]), precision=precision)
     return net, dec
 
 
-@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev"])
+@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev",
+                                  "gru_crisp_64_22_f512", "gru_polar_32_16_f128_noonehot"])
 def test_gru_decode_golden(name):
     d = golden(f"{name}.npz")
     net, dec = build(d)
@@ -114,3 +114,44 @@ def test_gru_bf16_ragged_matches_fp32_path():
     a = dec32.decode(net, False, y).cpu().numpy()
     b = dec3.decode(net, False, y).cpu().numpy()
     assert (a == b).all(1).mean() >= 0.99
+
+
+@pytest.mark.parametrize("N,F,L,onehot,B", [(64, 512, 2, True, 231), (128, 256, 1, True, 97), (32, 128, 2, False, 70),
+                                            (128, 512, 1, False, 40)])
+def test_gru_wide_vs_oracle(oracle, N, F, L, onehot, B):
+    """Hidden sizes 128-512 (weight-streaming kernel), 1 and 2 layers, ragged batches, vs the C oracle."""
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
+    code = reference_polar_code(N, N // 2)
+    torch.manual_seed(N + F + L)
+    net = RNN_Model("GRU", N + 1 + int(onehot), F, 1, L, N, 0, 0).to(DEV)
+    dec = RNN_decoder("y_input", N, code.info_positions, onehot=onehot)
+    _, _, y = code.mc_generate(B, 1.0, seed=5, device=DEV, want_msg=False)
+    out, logits = dec.decode(net, False, y, return_logits=True)
+    sd = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
+    od, ol = oracle.gru_decode(y.cpu().numpy(), sd, N, F, L, code.info_positions, onehot=onehot, want_logits=True)
+    out, logits = out.cpu().numpy(), logits.cpu().numpy()
+    same = (out == od).all(1)
+    assert same.mean() >= 0.97, same.mean()
+    err = np.abs(logits[same] - ol[same]).max()
+    assert err < LOGIT_ATOL, err
+
+
+def test_rnn_from_checkpoint_f512(tmp_path):
+    """A CRISP checkpoint as rnn_all.py saves it ({'net': state_dict, 'args': Namespace}, F = 512, 2 layers,
+    rev_polar K = 22 of target 22, onehot) loads with weights_only and decodes the fixture's words."""
+    import argparse
+    from neural_polar_decoder_amd.datasets import rnn_from_checkpoint
+    d = golden("gru_crisp_64_22_f512.npz")
+    sd = {k: torch.from_numpy(v) for k, v in gru_state_dict(d).items()}
+    args = argparse.Namespace(code="Polar", N=64, K=22, target_K=22, rate_profile="rev_polar", decoding_type="y_input",
+                              rnn_type="GRU", rnn_feature_size=512, rnn_depth=2, onehot=True, use_ynn=False,
+                              out_linear_depth=1, activation="selu", dropout=0.0)
+    path = tmp_path / "crisp.pt"
+    torch.save({"net": sd, "step": 100000, "args": args}, path)
+    net, dec, code = rnn_from_checkpoint(str(path))
+    assert np.array_equal(np.asarray(code.info_positions), d["info"])
+    out = dec.decode(net, False, torch.from_numpy(d["y"]).to(DEV)).cpu().numpy()
+    info = d["info"]
+    assert (out[:, info] == d["decoded"][:, info]).mean() >= 0.999
+    assert (out == d["decoded"]).all(1).mean() >= 0.99

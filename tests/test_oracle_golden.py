@@ -57,10 +57,12 @@ def test_error_counters_golden(oracle):
     assert bl / d["ref"].shape[0] == pytest.approx(float(d["bler"]), abs=0)
 
 
-@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev"])
+@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev",
+                                  "gru_crisp_64_22_f512", "gru_polar_32_16_f128_noonehot"])
 def test_gru_oracle_golden(oracle, name):
+    from conftest import gru_state_dict
     d = golden(f"{name}.npz")
-    sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    sd = gru_state_dict(d)
     dec, lg = oracle.gru_decode(d["y"], sd, int(d["N"]), int(d["F"]), 2, d["info"], onehot=bool(d["onehot"]),
                                 rev=bool(d["rev"]), want_logits=True)
     assert np.abs(lg - d["logits"]).max() < 1e-5
