@@ -294,6 +294,29 @@ def gru_leg(code, dev, y, B, world, timer):
             "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input, 2 dB, 2^20 per GPU"}
 
 
+def crisp_f512_leg(dev, rank, world, timer, B=1 << 15):
+    """The CRISP curriculum's decoder (run_crisp.sh): Polar(64,22) rev_polar profile, GRU hidden 512,
+    2 layers, onehot; fp32 weight-streaming MFMA kernel (weights 9.4 MB, read from L2/MALL each step)."""
+    import argparse as _ap
+    from neural_polar_decoder_amd import PolarCode
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    from neural_polar_decoder_amd.montecarlo import seeded_crisp
+    info = polar_info_positions(64, 22, "rev_polar", 22)
+    code = PolarCode(6, 22, _ap.Namespace(), F=np.setdiff1d(np.arange(64), info))
+    net, dec = seeded_crisp(code, 512, 2, seed=0, device=dev)
+    _, _, y = code.mc_generate(B, 0.0, SEED, 0, rank * B, device=dev, want_msg=False)
+    stream = torch.cuda.current_stream(dev)
+    t = timer(lambda: dec.decode(net, False, y), iters=1, warm=1)
+    ms = event_ms(lambda: dec.decode(net, False, y), 1, stream)
+    flop_cw = gru_flop_per_cw(64, 512)
+    tf = flop_cw * B / (ms / 1e3) / 1e12
+    return {"value": world * B / t, "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": ms,
+            "algorithmic_flop_per_cw": flop_cw, "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
+            "frac": tf / FP32_PEAK_TF, "dtype": "fp32 (v_mfma_f32_32x32x2_f32)",
+            "config": "run_crisp.sh decoder: Polar(64,22) rev_polar, CRISP GRU hidden 512, 2 layers, onehot, 0 dB, "
+                      "seeded untrained weights"}
+
+
 def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
     """configs[3]: PAC(128,64) (RM profile, g = 91), 2^20 codewords per GPU per SNR (2^23 over 8 GPUs),
     received words resident; CRISP GRU hidden 64 and PAC SC; one RCCL all-reduce of the counters."""
@@ -561,6 +584,7 @@ def main():
     if not args.no_gru:
         legs["sc_plus_gru"] = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg)
         legs["crisp_gru"] = gru_leg(code, dev, ys[2], B, world, timer)
+        legs["crisp_gru_f512"] = crisp_f512_leg(dev, rank, world, timer)
     if not (args.no_gru and args.no_pac):
         legs.update(pac_legs(snrs, B, rank, world, timer, dev, not args.no_gru, not args.no_pac))
     if not args.no_scl:
