@@ -80,7 +80,8 @@ typedef struct {
     float* bits; /* decoded_bits row */
 } lse_ctx;
 
-static inline float decide(const lse_ctx* c, float L) { return c->hard ? sgn(L) : tanhf(L / 2.0f); }
+static inline float decide_c(int hard, float L) { return hard ? sgn(L) : tanhf(L / 2.0f); }
+static inline float decide(const lse_ctx* c, float L) { return decide_c(c->hard, L); }
 
 /* decode(llrs, depth, bit_position) (polar.py:226-279); ret = returned partial-sum vector (2*half) */
 static void lse_decode(lse_ctx* c, const float* llrs, int depth, int bitpos, float* ret) {
@@ -131,6 +132,124 @@ void oracle_sc_decode_lse(const float* y, int64_t B, int N, int K, const int32_t
         if (bits_out) memcpy(bits_out + b * N, bits, sizeof(float) * (size_t)N);
         if (msg_hat)
             for (int k = 0; k < K; ++k) msg_hat[b * K + k] = sgn(bits[info[k]]);
+    }
+}
+
+/* ------------------------------------------------------------------ forward error bound of sc_decode */
+/*
+ * Running first-order error analysis of the same recursion (soft or hard decisions): alongside every
+ * fp32 value v the double E(v) bounds |v - v_exact| when every operation is evaluated with relative error
+ * at most eps_op: + - * and the LLR scaling are correctly rounded (1 unit of u = 2^-24); exp, log and
+ * tanh are allowed 4 units (2 ulp: glibc, Sleef -- torch's CPU path -- and the device OCML are all within
+ * that).  Propagation uses the exact sensitivities of each operation:
+ *   boxplus f(x,y) = log((1+e^(x+y))/(e^x+e^y)):  df/dx = s(x+y) - s(x-y), df/dy = s(x+y) - s(y-x)
+ *     (s = logistic), plus the rounding of its evaluated form log(1+e^(x+y)) - x - log(1+e^(y-x)),
+ *     whose terms have magnitude ~|x| + |y| (the cancellation that makes a leaf's LLR conditioning-bound);
+ *   g = u a + b;  tanh(L/2): 0.5 (1 - u^2);  partial-sum products u v.
+ * Two implementations that both satisfy the model differ by at most 2 E per value; tests use that as a
+ * per-entry bound on decoded_bits instead of a fixed tolerance.  Non-finite values (88 < x+y < 200: exp
+ * overflows and no patch applies) get an infinite bound (the tests compare those by NaN position).
+ */
+#define U32 5.9604644775390625e-08 /* 2^-24 */
+#define UT (4.0 * U32)             /* transcendental allowance */
+
+static inline double logistic(double t) { return 1.0 / (1.0 + exp(-t)); }
+/* m * e with 0 * inf = 0: an exactly known factor (error 0, or value 0) contributes nothing */
+static inline double sm(double m, double e) { return (m == 0.0 || e == 0.0) ? 0.0 : fabs(m) * e; }
+
+/* bound of u = tanh(L/2) given E(L): the tanh rounding plus the worst slope over [|L| - E, |L| + E];
+   L = +-inf (same patch branch on both sides) gives u = +-1 exactly */
+static inline double tanh_bound(float L, float u, double eL) {
+    if (!isfinite(L)) return 0.0;
+    if (!isfinite(eL)) return 1.0;
+    const double lo = fabs((double)L) - eL;
+    const double t = tanh((lo > 0.0 ? lo : 0.0) / 2.0);
+    return UT * fabs((double)u) + 0.5 * (1.0 - t * t) * eL;
+}
+
+static double lse_bound(float x, float y, float out, double ex, double ey) {
+    if (!isfinite(out)) return INFINITY;
+    const double xd = x, yd = y, s = xd + yd, d = yd - xd;
+    const double dfx = fabs(logistic(s) - logistic(xd - yd)), dfy = fabs(logistic(s) - logistic(d));
+    /* every branch (the plain formula, the |x+y| > 200 / |x-y| > 200 patches, the zero re-evaluation)
+       evaluates at most two log(1+e^t) terms and three subtractions on values of magnitude <= |x| + |y| */
+    const double t1 = s < 88.0 ? log1p(exp(s)) : s, t3 = d < 88.0 ? log1p(exp(d)) : d;
+    const double loc = U32 * (fabs(s) + fabs(d) + fabs(xd) + fabs(yd) + fabs((double)out)) + UT * (2.0 + t1 + t3);
+    return sm(dfx, ex) + sm(dfy, ey) + loc;
+}
+
+typedef struct {
+    int n;
+    const uint8_t* frozen;
+    int hard;
+    float* bits;
+    double* ebits;
+} lseb_ctx;
+
+static void lseb_decode(lseb_ctx* c, const float* llrs, const double* el, int depth, int bitpos, float* ret,
+                        double* eret) {
+    const int half = 1 << (c->n - depth - 1);
+    if (depth == c->n - 1) {
+        const int lp = 2 * bitpos, rp = 2 * bitpos + 1;
+        float u = 1.0f, v = 1.0f;
+        double eu = 0.0, ev = 0.0;
+        if (!c->frozen[lp]) {
+            float Lu;
+            log_sum_avoid_zero_nan(&llrs[0], &llrs[1], &Lu, 1);
+            const double eL = lse_bound(llrs[0], llrs[1], Lu, el[0], el[1]);
+            u = decide_c(c->hard, Lu);
+            eu = c->hard ? 0.0 : tanh_bound(Lu, u, eL);
+        }
+        if (!c->frozen[rp]) {
+            float Lv = u * llrs[0] + llrs[1];
+            const double eL = sm(llrs[0], eu) + sm(u, el[0]) + el[1] + U32 * (fabs((double)u * llrs[0]) + fabs((double)Lv));
+            v = decide_c(c->hard, Lv);
+            ev = c->hard ? 0.0 : tanh_bound(Lv, v, eL);
+        }
+        c->bits[lp] = u;
+        c->bits[rp] = v;
+        c->ebits[lp] = eu;
+        c->ebits[rp] = ev;
+        ret[0] = u * v;
+        eret[0] = sm(u, ev) + sm(v, eu) + U32 * fabs((double)ret[0]);
+        ret[1] = v;
+        eret[1] = ev;
+        return;
+    }
+    float Lu[LSE_MAX_N / 2], uh[LSE_MAX_N / 2], Lv[LSE_MAX_N / 2], vh[LSE_MAX_N / 2];
+    double eLu[LSE_MAX_N / 2], euh[LSE_MAX_N / 2], eLv[LSE_MAX_N / 2], evh[LSE_MAX_N / 2];
+    log_sum_avoid_zero_nan(llrs, llrs + half, Lu, half);
+    for (int j = 0; j < half; ++j) eLu[j] = lse_bound(llrs[j], llrs[half + j], Lu[j], el[j], el[half + j]);
+    lseb_decode(c, Lu, eLu, depth + 1, 2 * bitpos, uh, euh);
+    for (int j = 0; j < half; ++j) {
+        Lv[j] = uh[j] * llrs[j] + llrs[half + j];
+        eLv[j] = sm(llrs[j], euh[j]) + sm(uh[j], el[j]) + el[half + j] +
+                 U32 * (fabs((double)uh[j] * llrs[j]) + fabs((double)Lv[j]));
+    }
+    lseb_decode(c, Lv, eLv, depth + 1, 2 * bitpos + 1, vh, evh);
+    for (int j = 0; j < half; ++j) {
+        ret[j] = uh[j] * vh[j];
+        eret[j] = sm(uh[j], evh[j]) + sm(vh[j], euh[j]) + U32 * fabs((double)ret[j]);
+        ret[half + j] = vh[j];
+        eret[half + j] = evh[j];
+    }
+}
+
+/* decoded_bits (B,N) and their bounds ebits (B,N, double) */
+void oracle_sc_decode_lse_bound(const float* y, int64_t B, int N, const uint8_t* frozen, float llr_scale, int hard,
+                                float* bits_out, double* ebits_out) {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < B; ++b) {
+        float llr[LSE_MAX_N], ret[LSE_MAX_N];
+        double el[LSE_MAX_N], eret[LSE_MAX_N];
+        for (int i = 0; i < N; ++i) {
+            llr[i] = llr_scale * y[b * N + i];
+            el[i] = 0.0; /* one correctly rounded product, identical everywhere */
+        }
+        lseb_ctx c = {n, frozen, hard, bits_out + b * N, ebits_out + b * N};
+        lseb_decode(&c, llr, el, 0, 0, ret, eret);
     }
 }
 
@@ -190,5 +309,89 @@ void oracle_sc_decode_soft(const float* y, int64_t B, int N, int K, const int32_
         if (bits_out) memcpy(bits_out + b * N, bits, sizeof(float) * (size_t)N);
         if (msg_hat)
             for (int k = 0; k < K; ++k) msg_hat[b * K + k] = sgn(bits[info[k]]);
+    }
+}
+
+/* ------------------------------------------------------------------ forward error bound of sc_decode_soft */
+/* Same error model as oracle_sc_decode_lse_bound, on decode_soft's recursion (nodes return LLRs; leaves
+   clamp(L + prior, +-1000), which is 1-Lipschitz; bits = tanh(L/2) or sign(L)). */
+typedef struct {
+    int n;
+    const float* prior;
+    int hard;
+    float* bits;
+    double* ebits;
+} softb_ctx;
+
+static inline double add_bound(float a, float b, float r, double ea, double eb) {
+    (void)a; (void)b;
+    return ea + eb + U32 * fabs((double)r);
+}
+
+static void softb_decode(softb_ctx* c, const float* llrs, const double* el, int depth, int bitpos, float* ret,
+                         double* eret) {
+    const int half = 1 << (c->n - depth - 1);
+    if (depth == c->n - 1) {
+        const int lp = 2 * bitpos, rp = 2 * bitpos + 1;
+        float Lu0, Lu, Luv, Lv0, Lv, top;
+        log_sum_avoid_zero_nan(&llrs[0], &llrs[1], &Lu0, 1);
+        double eLu = lse_bound(llrs[0], llrs[1], Lu0, el[0], el[1]);
+        Lu = clamp1000(Lu0 + c->prior[lp] * 1.0f);
+        eLu = eLu + U32 * fabs((double)Lu0 + c->prior[lp]);
+        float u = c->hard ? sgn(Lu) : tanhf(Lu / 2.0f);
+        log_sum_avoid_zero_nan(&Lu, &llrs[0], &Luv, 1);
+        const double eLuv = lse_bound(Lu, llrs[0], Luv, eLu, el[0]);
+        Lv0 = Luv + llrs[1];
+        double eLv = add_bound(Luv, llrs[1], Lv0, eLuv, el[1]);
+        Lv = clamp1000(Lv0 + c->prior[rp] * 1.0f);
+        eLv = eLv + U32 * fabs((double)Lv0 + c->prior[rp]);
+        float v = c->hard ? sgn(Lv) : tanhf(Lv / 2.0f);
+        c->bits[lp] = u;
+        c->bits[rp] = v;
+        c->ebits[lp] = c->hard ? 0.0 : tanh_bound(Lu, u, eLu);
+        c->ebits[rp] = c->hard ? 0.0 : tanh_bound(Lv, v, eLv);
+        log_sum_avoid_zero_nan(&Lu, &Lv, &top, 1);
+        ret[0] = top;
+        eret[0] = lse_bound(Lu, Lv, top, eLu, eLv);
+        ret[1] = Lv;
+        eret[1] = eLv;
+        return;
+    }
+    float Lu[LSE_MAX_N / 2], Lhu[LSE_MAX_N / 2], Luv[LSE_MAX_N / 2], Lv[LSE_MAX_N / 2], Lhv[LSE_MAX_N / 2];
+    double eLu[LSE_MAX_N / 2], eLhu[LSE_MAX_N / 2], eLv[LSE_MAX_N / 2], eLhv[LSE_MAX_N / 2];
+    log_sum_avoid_zero_nan(llrs, llrs + half, Lu, half);
+    for (int j = 0; j < half; ++j) eLu[j] = lse_bound(llrs[j], llrs[half + j], Lu[j], el[j], el[half + j]);
+    softb_decode(c, Lu, eLu, depth + 1, 2 * bitpos, Lhu, eLhu);
+    log_sum_avoid_zero_nan(Lhu, llrs, Luv, half);
+    for (int j = 0; j < half; ++j) {
+        const double e = lse_bound(Lhu[j], llrs[j], Luv[j], eLhu[j], el[j]);
+        Lv[j] = Luv[j] + llrs[half + j];
+        eLv[j] = add_bound(Luv[j], llrs[half + j], Lv[j], e, el[half + j]);
+    }
+    softb_decode(c, Lv, eLv, depth + 1, 2 * bitpos + 1, Lhv, eLhv);
+    log_sum_avoid_zero_nan(Lhu, Lhv, ret, half);
+    for (int j = 0; j < half; ++j) {
+        eret[j] = lse_bound(Lhu[j], Lhv[j], ret[j], eLhu[j], eLhv[j]);
+        ret[half + j] = Lhv[j];
+        eret[half + j] = eLhv[j];
+    }
+}
+
+void oracle_sc_decode_soft_bound(const float* y, int64_t B, int N, const float* priors, float llr_scale, int hard,
+                                 float* bits_out, double* ebits_out) {
+    int n = 0;
+    while ((1 << n) < N) ++n;
+    float zeros[LSE_MAX_N] = {0};
+    const float* pr = priors ? priors : zeros;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < B; ++b) {
+        float llr[LSE_MAX_N], ret[LSE_MAX_N];
+        double el[LSE_MAX_N], eret[LSE_MAX_N];
+        for (int i = 0; i < N; ++i) {
+            llr[i] = llr_scale * y[b * N + i];
+            el[i] = 0.0;
+        }
+        softb_ctx c = {n, pr, hard, bits_out + b * N, ebits_out + b * N};
+        softb_decode(&c, llr, el, 0, 0, ret, eret);
     }
 }

@@ -1,14 +1,21 @@
-"""GPU parity of the exact-LSE SC decoder (npd_sc_decode_lse / PolarCode.sc_decode) against the
-reference's golden vectors (PolarCode.sc_decode, polar.py:209-279) and the C oracle
+"""GPU parity of the exact-LSE SC decoder (npd_sc_decode_lse / PolarCode.sc_decode) and the soft-output
+SC decoder (sc_decode_soft) against the reference's golden vectors (polar.py:209-358) and the C oracle
 (oracle/npd_oracle_lse.c).
 
-Tolerance: exp/log/tanh are the device libm on the GPU, glibc in the oracle and Sleef in torch's CPU
-path (each <= 1 ulp).  Hard decisions (args.hard_decision): >= 99.9 % of information bits and >= 99 %
-of codewords identical (measured: all).  Soft decisions (tanh(L/2), the reference's default) carry the
-ulp differences into every later partial sum, so a codeword whose decision sequence diverges once
-diverges in several bits: >= 99.5 % of bits and >= 98 % of codewords identical, decoded_bits: 99 %
-of entries within 1e-4 (measured 99.7 % at N = 256; soft partial sums multiply LLRs of magnitude
-~1e2, so a few entries drift up to ~0.06) on agreeing codewords where finite, the same NaN positions."""
+Tolerance, by analysis: exp/log/tanh are the device libm (OCML) on the GPU, glibc in the oracle and Sleef
+in torch's CPU path, each within 2 ulp.  The oracle propagates a first-order forward error bound E through
+the same recursion (oracle.sc_decode_lse_bound / sc_decode_soft_bound: exact sensitivities of the boxplus,
+of g = u a + b, of tanh(L/2) and of the partial-sum products, plus each operation's rounding), so two
+implementations of the model differ by at most 2 E per decoded_bits entry.  Soft partial sums multiply
+LLRs of magnitude ~1e2 (g = u a + b), so E reaches ~1e-2 on ill-conditioned entries -- the drifts up to
+~0.06 seen before were such entries.  Bars:
+  * hard decisions: >= 99.9 % of information bits and >= 99 % of codewords identical (measured: all);
+    decoded_bits bit-exact on agreeing codewords;
+  * soft decisions: >= 99.5 % of bits and >= 98 % of codewords identical; on agreeing codewords EVERY
+    finite decoded_bits entry within 2 E of the reference (max |diff| / 2E is reported), same NaN positions.
+Measured on MI355X (tools/lse_bound_report.py): max |diff| / 2E = 0.125 on every lse_* fixture (the
+oracle-vs-torch figure is the same), max |diff| 1.4e-4 (N = 128).
+"""
 import numpy as np
 import pytest
 import torch
@@ -18,7 +25,6 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 LSE_CASES = [(16, 8), (32, 16), (64, 32), (128, 64)]
-BITS_ATOL = 1e-4   # 99 % of soft decoded_bits entries
 
 
 def polar_for(N, info):
@@ -31,7 +37,8 @@ def t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-def check(hat, bits, ref_hat, ref_bits, hard, what):
+def check(hat, bits, ref_hat, ref_bits, hard, what, E=None):
+    """E: per-entry forward error bound of decoded_bits (required for soft decisions with bits)."""
     agree = hat == ref_hat
     bit_bar, row_bar = (0.999, 0.99) if hard else (0.995, 0.98)
     assert agree.mean() >= bit_bar and agree.all(axis=1).mean() >= row_bar, (what, agree.mean(),
@@ -43,8 +50,21 @@ def check(hat, bits, ref_hat, ref_bits, hard, what):
         if hard:
             assert np.array_equal(bits[rows][fin], ref_bits[rows][fin]), what
         else:
-            err = np.abs(bits[rows][fin] - ref_bits[rows][fin])
-            assert (err <= BITS_ATOL).mean() >= 0.99, (what, (err <= BITS_ATOL).mean(), err.max(initial=0.0))
+            err = np.abs(bits[rows][fin].astype(np.float64) - ref_bits[rows][fin])
+            bound = 2.0 * E[rows][fin]
+            ratio = err / np.maximum(bound, 1e-300)
+            assert np.all(err <= bound), (what, "max |diff| / 2E", float(ratio.max(initial=0.0)),
+                                          "max |diff|", float(err.max(initial=0.0)))
+
+
+def lse_bound(y, snr, info):
+    from oracle import oracle as O
+    return O.sc_decode_lse_bound(y, snr, info, False)[1]
+
+
+def soft_bound(y, snr, prior):
+    from oracle import oracle as O
+    return O.sc_decode_soft_bound(y, snr, False, prior)[1]
 
 
 @pytest.mark.parametrize("N,K", LSE_CASES)
@@ -54,11 +74,13 @@ def test_sc_decode_lse_golden(N, K):
     for tag, hard in (("hard", True), ("soft", False)):
         hat = np.empty_like(d[f"msg_hat_{tag}"])
         bits = np.empty_like(d[f"bits_{tag}"])
+        E = np.empty(bits.shape, np.float64)
         for s in np.unique(d["snr"]):
             m = d["snr"] == s
             h, b = code.sc_decode(t(d["y"][m]), float(s), hard_decision=hard, return_bits=True)
             hat[m], bits[m] = h.cpu().numpy(), b.cpu().numpy()
-        check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag))
+            E[m] = lse_bound(d["y"][m], float(s), d["info"])
+        check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag), E)
 
 
 def test_sc_decode_lse_args_default_is_soft():
@@ -89,7 +111,7 @@ def test_sc_decode_lse_vs_oracle_random(oracle, N, K):
         for hard in (True, False):
             h, b = code.sc_decode(t(y), 2.5, hard_decision=hard, return_bits=True)
             oh, ob = oracle.sc_decode_lse(y, 2.5, info, hard)
-            check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard))
+            check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), lse_bound(y, 2.5, info))
 
 
 def test_sc_decode_lse_full_size_properties(oracle):
@@ -156,13 +178,15 @@ def test_sc_decode_soft_golden(N, K):
             tag = ("hard" if hard else "soft") + "_" + ptag
             hat = np.empty_like(d[f"msg_hat_{tag}"])
             bits = np.empty_like(d[f"bits_{tag}"])
+            E = np.empty(bits.shape, np.float64)
             for s in np.unique(d["snr"]):
                 m = d["snr"] == s
-                h, b = code.sc_decode_soft(t(d["y"][m]), float(s), priors=None if ptag == "p0" else d["prior"],
-                                           hard_decision=hard, return_bits=True)
+                pr = None if ptag == "p0" else d["prior"]
+                h, b = code.sc_decode_soft(t(d["y"][m]), float(s), priors=pr, hard_decision=hard, return_bits=True)
                 hat[m], bits[m] = h.cpu().numpy(), b.cpu().numpy()
+                E[m] = soft_bound(d["y"][m], float(s), pr)
             if ptag == "pr":
-                check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag))
+                check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag), E)
             else:
                 ag = hat == d[f"msg_hat_{tag}"]
                 assert ag.mean() >= 0.995 and ag.all(axis=1).mean() >= 0.98, (N, tag)
@@ -183,4 +207,4 @@ def test_sc_decode_soft_vs_oracle_random(oracle):
             for hard in (True, False):
                 h, b = code.sc_decode_soft(t(y), 2.5, priors=prior, hard_decision=hard, return_bits=True)
                 oh, ob = oracle.sc_decode_soft(y, 2.5, info, hard, prior)
-                check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard))
+                check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), soft_bound(y, 2.5, prior))
