@@ -12,7 +12,8 @@
 //   * FC layers = LDS-tiled GEMM with MFMA rows = codewords, columns = output features (so the
 //     epilogue writes contiguous feature runs), bias + GELU fused.
 //   * LayerNorm + sign: one wave per codeword.
-// Activations of a chunk of codewords live in a caller-provided workspace (row-major (B, C, N)).
+// Activations of a chunk of codewords live in a caller-provided workspace, (B, N, C) (channels
+// contiguous); FC0's weights are permuted on the host to that flatten order.
 #include <math.h>
 #include <string.h>
 
@@ -45,63 +46,93 @@ __device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
 }
 
 // ------------------------------------------------------------------------------ conv layer
-// grid: (N/64 position tiles, cout/64 channel tiles, codewords); block 256 = 2 (co) x 2 (pos) waves
+// Activations are (B, N, C) -- channels contiguous per position -- so a block's input slab (64 positions
+// plus the dilation halo, all channels) is one contiguous run in HBM (16-B loads) and lands in LDS as
+// [position][channel] rows of stride CS = cin + 4 (16-B aligned, conflict-free ds_read_b128 across the
+// 32 position columns of a wave).  MFMA k-steps run tap by tap; within tap t, k-step s pairs channel s
+// (lane half 0) with channel s + cin/2 (half 1), so the B operands of 4 consecutive k-steps are one
+// ds_read_b128 and the A operands (weights, permuted on the host in the same order) one 16-B load.
+// The accumulator's registers 4q..4q+3 hold 4 consecutive output channels of one position: bias, GELU,
+// residual and the store are 16-B vectors.  Layer 0 (cin = 1): the 7 taps are the k-steps (padded to 8).
+// grid: (N/64 position tiles, cout_pad/64 channel tiles, codewords); block 256 = 2 (co) x 2 (pos) waves.
+template <bool CIN1>
 __global__ __launch_bounds__(256) void conv_layer_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                          const float* __restrict__ res, const float* __restrict__ wimg,
                                                          const float* __restrict__ bias, int cin, int cout, int N,
-                                                         int dil, int ksteps, int do_res) {
+                                                         int dil, int do_res) {
     extern __shared__ __attribute__((aligned(16))) float slab[];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int l0 = blockIdx.x * 64;
-    const int co_tile = blockIdx.y;  // 64 output channels
     const int64_t b = blockIdx.z;
     const int halo = 3 * dil;
     const int W = 64 + 2 * halo;
-    const int WS = W + 1;
-    const float* inb = in + b * (int64_t)cin * N;
-    for (int e = tid; e < cin * W; e += 256) {
-        const int ci = e / W, p = e - ci * W;
-        const int l = l0 - halo + p;
-        slab[ci * WS + p] = (l >= 0 && l < N) ? inb[(int64_t)ci * N + l] : 0.0f;
+    const int CS = CIN1 ? 4 : cin + 4;
+    if constexpr (CIN1) {
+        const float* inb = in + b * (int64_t)N;
+        for (int p = tid; p < W; p += 256) {
+            const int l = l0 - halo + p;
+            slab[p * CS] = (l >= 0 && l < N) ? inb[l] : 0.0f;
+        }
+    } else {
+        const int c4n = cin >> 2;
+        const f4* inb = reinterpret_cast<const f4*>(in + b * (int64_t)N * cin);
+        for (int e = tid; e < W * c4n; e += 256) {
+            const int p = e / c4n, c4 = e - p * c4n;
+            const int l = l0 - halo + p;
+            const f4 v = (l >= 0 && l < N) ? inb[(int64_t)l * c4n + c4] : f4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<f4*>(slab + p * CS + 4 * c4) = v;
+        }
     }
     __syncthreads();
     const int co_sub = wave & 1, pos_sub = wave >> 1;
-    const int co_t32 = co_tile * 2 + co_sub;  // 32-channel tile index
-    const f4* wq = reinterpret_cast<const f4*>(wimg) + (int64_t)co_t32 * ((ksteps + 3) / 4) * 64 + lane;
-    f16v acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    // lane's running (tap, channel) of k = 2s + h
-    int t = 0, ci = h;
-    while (ci >= cin) { ci -= cin; ++t; }
+    const int co_t32 = blockIdx.y * 2 + co_sub;  // 32-channel tile index
     const int pcol = pos_sub * 32 + col;
-    const int ng = (ksteps + 3) / 4;
-    f4 wn = wq[0];
-    for (int g = 0; g < ng; ++g) {
-        const f4 w = wn;
-        if (g + 1 < ng) wn = wq[(g + 1) * 64];
+    f16v acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (CIN1) {
+        const f4 w = reinterpret_cast<const f4*>(wimg)[co_t32 * 64 + lane];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const bool valid = t < 7;
-            const float bv = valid ? slab[ci * WS + pcol + dil * t] : 0.0f;
-            acc = mfma(w[e], bv, acc);
-            ci += 2;
-            while (ci >= cin) {
-                ci -= cin;
-                ++t;
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const int t = 2 * s2 + h;
+            const float bv = t < 7 ? slab[(pcol + dil * t) * CS] : 0.0f;
+            acc = mfma(w[s2], bv, acc);
+        }
+    } else {
+        const int ng = cin >> 3;  // groups of 4 k-steps per tap
+        const f4* wq = reinterpret_cast<const f4*>(wimg) + (int64_t)co_t32 * 7 * ng * 64 + lane;
+        f4 wn = wq[0];
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const f4* brow = reinterpret_cast<const f4*>(slab + (pcol + dil * t) * CS + h * (cin >> 1));
+            for (int g = 0; g < ng; ++g) {
+                const f4 w = wn;
+                const int nxt = t * ng + g + 1;
+                if (nxt < 7 * ng) wn = wq[nxt * 64];
+                const f4 bv = brow[g];
+                acc = mfma(w.x, bv.x, acc);
+                acc = mfma(w.y, bv.y, acc);
+                acc = mfma(w.z, bv.z, acc);
+                acc = mfma(w.w, bv.w, acc);
             }
         }
     }
-    // epilogue: rows = channels, columns = positions
+    // epilogue: registers 4q..4q+3 = channels co_t32*32 + 8q + 4h + 0..3 at position l0 + pcol
+    const int l = l0 + pcol;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int co = co_t32 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int l = l0 + pcol;
+    for (int q = 0; q < 4; ++q) {
+        const int co = co_t32 * 32 + 8 * q + 4 * h;
         if (co < cout) {
-            const int64_t o = (b * cout + co) * (int64_t)N + l;
-            float v = gelu(acc[r] + bias[co]);
-            if (do_res) v += res[o];
-            out[o] = v;
+            const int64_t o = (b * N + l) * (int64_t)cout + co;
+            const f4 bb = *reinterpret_cast<const f4*>(bias + co);
+            f4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu(acc[4 * q + e] + bb[e]);
+            if (do_res) {
+                const f4 rv = *reinterpret_cast<const f4*>(res + o);
+                v += rv;
+            }
+            *reinterpret_cast<f4*>(out + o) = v;
         }
     }
 }
@@ -220,7 +251,7 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
     *out = nullptr;
     NPD_ARG(weights != nullptr, "npd_conv_create: weights is NULL");
     NPD_ARG(N >= 64 && N <= 1024 && N % 64 == 0, "npd_conv_create: N must be a multiple of 64 in [64, 1024]");
-    NPD_ARG(embed >= 2 && embed <= 512 && embed % 2 == 0, "npd_conv_create: embed must be even, in [2, 512]");
+    NPD_ARG(embed >= 16 && embed <= 512 && embed % 16 == 0, "npd_conv_create: embed must be a multiple of 16 in [16, 512]");
     NPD_ARG(precision == 0, "npd_conv_create: only fp32 (precision 0) is built");
     const int E = embed;
     // host weights in state_dict order: (w, b) per conv layer, then 3 x (w, b) Linear, then LN (g, b)
@@ -246,35 +277,56 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
         LayerDesc& L = c->layers[i];
         L.cin = ci; L.cout = co; L.dil = d; L.res = r;
         L.ksteps = (7 * ci + 1) / 2;
-        const int ng = (L.ksteps + 3) / 4;
         // pad channel tiles to 64 so every (64-channel) block has two 32-row MFMA tiles
         const int co_pad = ((co + 63) / 64) * 64;
+        while (img.size() % 4) img.push_back(0.0f);
         L.woff = (int64_t)img.size();
-        img.resize(img.size() + (size_t)(co_pad / 32) * ng * 64 * 4, 0.0f);
         const float* w = p;  // (co, ci, 7)
-        for (int t32 = 0; t32 < co_pad / 32; ++t32)
-            for (int s = 0; s < L.ksteps; ++s)
-                for (int l = 0; l < 64; ++l) {
-                    const int row = 32 * t32 + (l & 31);
-                    const int k = 2 * s + (l >> 5);
-                    float v = 0.0f;
-                    if (row < co && k < 7 * ci) {
-                        const int t = k / ci, cc = k % ci;
-                        v = w[((int64_t)row * ci + cc) * 7 + t];
+        if (ci == 1) {
+            // [t32][lane][4]: k-step s of lane half hh is tap 2s + hh (tap 7 = 0)
+            img.resize(img.size() + (size_t)(co_pad / 32) * 64 * 4, 0.0f);
+            for (int t32 = 0; t32 < co_pad / 32; ++t32)
+                for (int l = 0; l < 64; ++l)
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        const int row = 32 * t32 + (l & 31), t = 2 * s2 + (l >> 5);
+                        img[L.woff + ((int64_t)t32 * 64 + l) * 4 + s2] = (row < co && t < 7) ? w[(int64_t)row * 7 + t] : 0.0f;
                     }
-                    img[L.woff + (((int64_t)t32 * ng + s / 4) * 64 + l) * 4 + (s & 3)] = v;
-                }
+        } else {
+            // [t32][tap][group][lane][4]: k-step 4g+e of tap t pairs channel 4g+e (half 0) with cin/2 + 4g+e
+            const int ng = ci / 8;
+            img.resize(img.size() + (size_t)(co_pad / 32) * 7 * ng * 64 * 4, 0.0f);
+            for (int t32 = 0; t32 < co_pad / 32; ++t32)
+                for (int t = 0; t < 7; ++t)
+                    for (int g = 0; g < ng; ++g)
+                        for (int l = 0; l < 64; ++l)
+                            for (int e = 0; e < 4; ++e) {
+                                const int row = 32 * t32 + (l & 31);
+                                const int cc = (l >> 5) * (ci / 2) + 4 * g + e;
+                                img[L.woff + ((((int64_t)t32 * 7 + t) * ng + g) * 64 + l) * 4 + e] =
+                                    row < co ? w[((int64_t)row * ci + cc) * 7 + t] : 0.0f;
+                            }
+        }
         p += (int64_t)co * ci * 7;
         L.boff = (int64_t)img.size();
         img.insert(img.end(), p, p + co);
         img.resize(L.boff + co_pad, 0.0f);
+        while (img.size() % 4) img.push_back(0.0f);
         p += co;
     }
     const int64_t fcin[3] = {(int64_t)E * N, 4 * N, N}, fcout[3] = {4 * N, N, N};
     for (int f = 0; f < 3; ++f) {
         while (img.size() % 4) img.push_back(0.0f);  // 16-B alignment for f4 loads
         c->off_fc[f][0] = (int64_t)img.size();
-        img.insert(img.end(), p, p + fcin[f] * fcout[f]);
+        if (f == 0) {
+            // the activations are (B, N, E): flatten index l*E + c instead of torch's c*N + l
+            const size_t base = img.size();
+            img.resize(base + (size_t)fcin[0] * fcout[0]);
+            for (int64_t j = 0; j < fcout[0]; ++j)
+                for (int cc = 0; cc < E; ++cc)
+                    for (int l = 0; l < N; ++l) img[base + j * fcin[0] + (int64_t)l * E + cc] = p[j * fcin[0] + (int64_t)cc * N + l];
+        } else {
+            img.insert(img.end(), p, p + fcin[f] * fcout[f]);
+        }
         p += fcin[f] * fcout[f];
         c->off_fc[f][1] = (int64_t)img.size();
         img.insert(img.end(), p, p + fcout[f]);
@@ -332,7 +384,8 @@ extern "C" int npd_conv_forward(const npd_conv* c, const float* y, float* logits
     float* H3 = H2 + Bc * (int64_t)N;
     static bool attr = false;
     if (!attr) {
-        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    163840));
         attr = true;
     }
     for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -353,10 +406,14 @@ extern "C" int npd_conv_forward(const npd_conv* c, const float* y, float* logits
             float* o = bufs[out_idx];
             const float* rsrc = L.res ? bufs[res_idx] : nullptr;
             const int halo = 3 * L.dil;
-            const size_t lds = (size_t)L.cin * (64 + 2 * halo + 1) * 4;
+            const size_t lds = (size_t)(L.cin == 1 ? 4 : L.cin + 4) * (64 + 2 * halo) * 4;
             dim3 grid(N / 64, (L.cout + 63) / 64, (unsigned)nb);
-            hipLaunchKernelGGL(conv_layer_kernel, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff, c->img + L.boff,
-                               L.cin, L.cout, N, L.dil, L.ksteps, L.res);
+            if (L.cin == 1)
+                hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
+                                   c->img + L.boff, L.cin, L.cout, N, L.dil, L.res);
+            else
+                hipLaunchKernelGGL(conv_layer_kernel<false>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
+                                   c->img + L.boff, L.cin, L.cout, N, L.dil, L.res);
             int rc = launch_check("conv_layer_kernel launch");
             if (rc) return rc;
             // block structure (models.py:742-766): the output of layers1 (i == 1) and of each residual
@@ -364,7 +421,7 @@ extern "C" int npd_conv_forward(const npd_conv* c, const float* y, float* logits
             if (i == 1 || i == 3 || i == 5 || i == 7) res_idx = out_idx;
             in_idx = out_idx;
         }
-        const float* flat = bufs[in_idx];  // (nb, E*N): c*N + l, as torch.flatten(start_dim=1)
+        const float* flat = bufs[in_idx];  // (nb, N*E): l*E + c (FC0's weights are permuted to match)
         const int64_t K1 = (int64_t)E * N;
         dim3 g1(4 * N / 64, (unsigned)((nb + 63) / 64));
         hipLaunchKernelGGL(fc_kernel, g1, dim3(256), 0, s, flat, c->img + c->off_fc[0][0], c->img + c->off_fc[0][1], H1,

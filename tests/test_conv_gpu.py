@@ -1,9 +1,12 @@
 """GPU parity of the fused convNet decoder (npd_conv_forward) against the reference's convNet.forward
 logits (golden) and the float64 numpy oracle.
 
-Tolerance (fp32 MFMA vs PyTorch CPU fp32, different summation order through 10 conv layers, 3 FC
-layers and LayerNorm): logits within 1e-3 absolute (LayerNorm output is O(1)); decisions
-(sign) identical except where the reference logit is within 1e-3 of zero.
+Tolerance (fp32 MFMA vs PyTorch CPU fp32: same operations, different summation order through 10 conv
+layers (dot products of up to 7 x 128 terms), 3 FC layers (up to 32768 terms) and LayerNorm): logits
+within 1e-5 absolute (LayerNorm output is O(1), |logit| <= 2.3 on the C5 fixture; sqrt(32768) x 2^-24 x
+O(1) ~ 1e-5 bounds the typical accumulated rounding); decisions (sign) identical except where the
+reference logit is within 1e-5 of zero.  Measured on MI355X (tools/conv_err_report.py): max |diff| =
+4.8e-7 (embed 16, N 64, vs reference), 3.6e-7 (vs oracle), 6.0e-7 (C5: embed 128, N 256).
 """
 import argparse
 
@@ -15,7 +18,7 @@ from conftest import conv_weights_from_seed, golden
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-ATOL = 1e-3
+ATOL = 1e-5
 
 
 def net_from(sd, embed, N):
@@ -27,7 +30,8 @@ def net_from(sd, embed, N):
 
 
 def check(lg, dec, ref_lg):
-    assert np.abs(lg - ref_lg).max() < ATOL, np.abs(lg - ref_lg).max()
+    err = np.abs(lg - ref_lg).max()
+    assert err < ATOL, ("max |logit diff|", float(err))
     sure = np.abs(ref_lg) > ATOL
     assert np.array_equal(dec[sure], np.sign(ref_lg)[sure])
 
