@@ -122,8 +122,8 @@ int npd_sc_decode_lse(const npd_code* code, const float* y, float llr_scale, int
  * Soft-output SC, PolarCode.sc_decode_soft(noisy_code, snr, priors) (polar.py:281-358): LSE check
  * nodes, leaf L^ = clamp(L + prior, -1000, 1000), right-child input LSE(L^_left, L_a) + L_b, nodes
  * return [LSE(L^_u, L^_v), L^_v]; frozen positions get no special treatment (priors carry them).
- * priors: HOST array of N floats or NULL (zeros).  Outputs as npd_sc_decode_lse.  N <= 64, y 16-byte
- * aligned.
+ * priors: HOST array of N floats or NULL (zeros).  Outputs as npd_sc_decode_lse.  4 <= N <= 256, y
+ * 16-byte aligned.
  */
 int npd_sc_decode_soft(const npd_code* code, const float* y, float llr_scale, int hard_decision, const float* priors,
                        float* msg_hat, float* u_bits, int64_t B, void* stream);
@@ -135,7 +135,7 @@ int npd_sc_decode_soft(const npd_code* code, const float* y, float llr_scale, in
  * LLRs), path metric += |leaf| on a frozen leaf with sign(leaf) != 1 and on the flipped branch of an
  * information leaf; survivors = torch.topk's choice (ties resolved exactly as std::nth_element, see
  * npd_list_prune_select) in list order; final path = the first minimum of ||encode(u) - y||^2.
- * Polar codes, 8 <= N <= 64, 1 <= list_size <= 8, y 16-byte aligned.  Outputs: msg_hat (B,K) and
+ * Polar codes, 8 <= N <= 256, 1 <= list_size <= 8, y 16-byte aligned.  Outputs: msg_hat (B,K) and
  * u_hat (B,N) of the chosen path, each optional.  scl_decode's leaf-LLR output equals
  * npd_sc_decode(..., gt = u_hat) (a genie pass reproduces the chosen path's LLRs bit for bit).
  * Decisions are bit-exact with the reference except when two list candidates' fp32 distances differ

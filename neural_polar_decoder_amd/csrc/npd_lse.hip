@@ -274,7 +274,8 @@ static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
 // PolarCode.sc_decode_soft / decode_soft (polar.py:281-358): the same tree, but every node returns LLRs
 // instead of partial sums -- leaf: L^ = clamp(L + prior, -1000, 1000) (utils.py:259-263 with the 1e-10
 // margins vanishing in fp32), decided sign/tanh; right child input LSE(L^_left, L_a) + L_b; node return
-// [LSE(L^_u, L^_v), L^_v].  No frozen handling (priors carry it).  N <= 64, register-resident.
+// [LSE(L^_u, L^_v), L^_v].  No frozen handling (priors carry it).  N <= 64: register-resident;
+// N = 128, 256: LDS-resident iterative walk (lse_soft_lds_kernel, the layout of lse_sc_kernel).
 struct SoftArgs {
     const float* y;
     float* msg;
@@ -282,7 +283,7 @@ struct SoftArgs {
     int64_t B;
     int64_t ntiles;
     float scale;
-    float prior[64];
+    float prior[kMaxN];
 };
 
 __device__ __forceinline__ float clamp1000(float x) { return x < -1000.0f ? -1000.0f : (x > 1000.0f ? 1000.0f : x); }
@@ -348,6 +349,84 @@ static int launch_soft(const CodeParams& p, SoftArgs a, hipStream_t stream) {
     return launch_check("lse_soft_sc_kernel launch");
 }
 
+// N >= 128: per-lane LLR levels (N-1 floats) and returned LLRs (N floats) in LDS, lane-interleaved; the
+// schedule of lse_sc_kernel with decode_soft's node rules: right-child input LSE(L^_left, L_a) + L_b,
+// node return [LSE(L^_u, L^_v), L^_v] combined in place when a node's right child finishes.
+template <bool SOFT>
+__global__ __launch_bounds__(64) void lse_soft_lds_kernel(const CodeParams p, const SoftArgs a) {
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x;
+    const int N = p.N, n = p.n, K = p.K;
+    float* const L = lds + lane;              // LLR level with 2^d values at elements [2^d - 1, 2^(d+1) - 1)
+    float* const beta = L + (N - 1) * kWave;  // returned LLRs L^, N values
+#define LV(base, j) (L[((base) + (j)) * kWave])
+#define BT(j) (beta[(j) * kWave])
+    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int64_t row = t * kWave + lane;
+        const bool valid = row < a.B;
+        const int64_t r = valid ? row : a.B - 1;
+        const float* yr = a.y + r * N;
+        float* ub = (a.ubits && valid) ? a.ubits + row * N : nullptr;
+        float* mh = (a.msg && valid) ? a.msg + row * K : nullptr;
+        for (int i = 0; i < N; ++i) {
+            int d;
+            if (i == 0) {
+                const int h = N >> 1;
+                for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_f(rmul(a.scale, yr[j]), rmul(a.scale, yr[j + h]));
+                d = n - 1;
+            } else {
+                const int k = __builtin_ctz((unsigned)i);
+                const int h = 1 << k;
+                const int s = i - h;
+                if (k + 1 == n) {
+                    for (int j = 0; j < h; ++j)
+                        LV(h - 1, j) = lse_f(BT(s + j), rmul(a.scale, yr[j])) + rmul(a.scale, yr[j + h]);
+                } else {
+                    for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_f(BT(s + j), LV(2 * h - 1, j)) + LV(2 * h - 1, j + h);
+                }
+                d = k;
+            }
+            for (int dd = d; dd >= 1; --dd) {
+                const int h = 1 << (dd - 1);
+                for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_f(LV(2 * h - 1, j), LV(2 * h - 1, j + h));
+            }
+            const float Lf = clamp1000(LV(0, 0) + a.prior[i]);
+            const float u = SOFT ? tanhf(Lf * 0.5f) : sgnf(Lf);
+            BT(i) = Lf;
+            if (ub) ub[i] = u;
+            const bool frozen = (p.frozen[i >> 5] >> (i & 31)) & 1u;
+            if (mh && !frozen) mh[p.rank[i]] = sgnf(u);
+            for (int l = 1; l < n && ((i + 1) & ((1 << l) - 1)) == 0; ++l) {
+                const int h = 1 << (l - 1);
+                const int s = i + 1 - (1 << l);
+                for (int j = 0; j < h; ++j) BT(s + j) = lse_f(BT(s + j), BT(s + h + j));
+            }
+        }
+    }
+#undef LV
+#undef BT
+}
+
+template <bool SOFT>
+static int launch_soft_lds(const CodeParams& p, SoftArgs a, hipStream_t stream) {
+    const size_t lds = (size_t)(2 * p.N - 1) * kWave * sizeof(float);
+    auto kern = lse_soft_lds_kernel<SOFT>;
+    static bool attr_set = false;  // benign race (idempotent)
+    if (!attr_set && lds > 65536) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr_set = true;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kWave, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    a.ntiles = (a.B + kWave - 1) / kWave;
+    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), lds, stream, p, a);
+    return launch_check("lse_soft_lds_kernel launch");
+}
+
 template <bool SOFT>
 static int dispatch_soft(const CodeParams& p, const SoftArgs& a, hipStream_t s) {
     switch (p.N) {
@@ -356,7 +435,7 @@ static int dispatch_soft(const CodeParams& p, const SoftArgs& a, hipStream_t s) 
         case 16: return launch_soft<16, SOFT>(p, a, s);
         case 32: return launch_soft<32, SOFT>(p, a, s);
         case 64: return launch_soft<64, SOFT>(p, a, s);
-        default: return fail(NPD_EINVAL, "npd_sc_decode_soft: N <= 64");
+        default: return launch_soft_lds<SOFT>(p, a, s);
     }
 }
 
@@ -391,7 +470,7 @@ extern "C" int npd_sc_decode_soft(const npd_code* code, const float* y, float ll
                                   const float* priors, float* msg_hat, float* u_bits, int64_t B, void* stream) {
     NPD_ARG(code != nullptr, "npd_sc_decode_soft: code is NULL");
     NPD_ARG(!code->p.pac, "npd_sc_decode_soft: Polar codes only (PolarCode.sc_decode_soft)");
-    NPD_ARG(code->p.N <= 64, "npd_sc_decode_soft: N <= 64");
+    NPD_ARG(code->p.N >= 4 && code->p.N <= kMaxN, "npd_sc_decode_soft: 4 <= N <= 256");
     NPD_ARG(B >= 0, "npd_sc_decode_soft: B < 0");
     NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_soft: y is NULL");
     NPD_ARG(((uintptr_t)y & 15u) == 0, "npd_sc_decode_soft: y must be 16-byte aligned");
@@ -402,7 +481,7 @@ extern "C" int npd_sc_decode_soft(const npd_code* code, const float* y, float ll
     a.ubits = u_bits;
     a.B = B;
     a.scale = llr_scale;
-    for (int i = 0; i < 64; ++i) a.prior[i] = (priors && i < code->p.N) ? priors[i] : 0.0f;
+    for (int i = 0; i < kMaxN; ++i) a.prior[i] = (priors && i < code->p.N) ? priors[i] : 0.0f;
     return hard_decision ? lse::dispatch_soft<false>(code->p, a, (hipStream_t)stream)
                          : lse::dispatch_soft<true>(code->p, a, (hipStream_t)stream);
 }

@@ -225,7 +225,7 @@ class PolarCode:
     def sc_decode_soft(self, noisy_code, snr, priors=None, hard_decision=None, return_bits=False):
         """PolarCode.sc_decode_soft (polar.py:281-358): soft-output SC -- every node returns LLRs
         (LSE(L^_u, L^_v), L^_v), leaves clamp(L + prior, +-1000); frozen positions are not special (the
-        priors carry them, as in the reference).  Returns sign(decoded_bits)[:, info] (B,K).  N <= 64."""
+        priors carry them, as in the reference).  Returns sign(decoded_bits)[:, info] (B,K).  N <= 256."""
         if hard_decision is None:
             hard_decision = bool(getattr(self.args, "hard_decision", False)) if self.args is not None else False
         y = _aligned(_lib.f32c(_lib.stage(noisy_code, "noisy_code")))

@@ -184,7 +184,16 @@ typedef struct {
     int hard;
     float* bits;
     double* ebits;
+    float* leaf;    /* decision LLR of every leaf (frozen leaves: NaN), or NULL */
+    double* eleaf;  /* its bound */
 } lseb_ctx;
+
+static inline void put_leaf(float* leaf, double* eleaf, int pos, float L, double e) {
+    if (leaf) {
+        leaf[pos] = L;
+        eleaf[pos] = e;
+    }
+}
 
 static void lseb_decode(lseb_ctx* c, const float* llrs, const double* el, int depth, int bitpos, float* ret,
                         double* eret) {
@@ -199,12 +208,18 @@ static void lseb_decode(lseb_ctx* c, const float* llrs, const double* el, int de
             const double eL = lse_bound(llrs[0], llrs[1], Lu, el[0], el[1]);
             u = decide_c(c->hard, Lu);
             eu = c->hard ? 0.0 : tanh_bound(Lu, u, eL);
+            put_leaf(c->leaf, c->eleaf, lp, Lu, eL);
+        } else {
+            put_leaf(c->leaf, c->eleaf, lp, NAN, 0.0);
         }
         if (!c->frozen[rp]) {
             float Lv = u * llrs[0] + llrs[1];
             const double eL = sm(llrs[0], eu) + sm(u, el[0]) + el[1] + U32 * (fabs((double)u * llrs[0]) + fabs((double)Lv));
             v = decide_c(c->hard, Lv);
             ev = c->hard ? 0.0 : tanh_bound(Lv, v, eL);
+            put_leaf(c->leaf, c->eleaf, rp, Lv, eL);
+        } else {
+            put_leaf(c->leaf, c->eleaf, rp, NAN, 0.0);
         }
         c->bits[lp] = u;
         c->bits[rp] = v;
@@ -235,9 +250,10 @@ static void lseb_decode(lseb_ctx* c, const float* llrs, const double* el, int de
     }
 }
 
-/* decoded_bits (B,N) and their bounds ebits (B,N, double) */
+/* decoded_bits (B,N) and their bounds ebits (B,N, double); optionally each leaf's decision LLR and its
+   bound (B,N; frozen leaves NaN / 0) */
 void oracle_sc_decode_lse_bound(const float* y, int64_t B, int N, const uint8_t* frozen, float llr_scale, int hard,
-                                float* bits_out, double* ebits_out) {
+                                float* bits_out, double* ebits_out, float* leaf_out, double* eleaf_out) {
     int n = 0;
     while ((1 << n) < N) ++n;
 #pragma omp parallel for schedule(static)
@@ -248,7 +264,8 @@ void oracle_sc_decode_lse_bound(const float* y, int64_t B, int N, const uint8_t*
             llr[i] = llr_scale * y[b * N + i];
             el[i] = 0.0; /* one correctly rounded product, identical everywhere */
         }
-        lseb_ctx c = {n, frozen, hard, bits_out + b * N, ebits_out + b * N};
+        lseb_ctx c = {n, frozen, hard, bits_out + b * N, ebits_out + b * N, leaf_out ? leaf_out + b * N : NULL,
+                      eleaf_out ? eleaf_out + b * N : NULL};
         lseb_decode(&c, llr, el, 0, 0, ret, eret);
     }
 }
@@ -321,6 +338,8 @@ typedef struct {
     int hard;
     float* bits;
     double* ebits;
+    float* leaf;
+    double* eleaf;
 } softb_ctx;
 
 static inline double add_bound(float a, float b, float r, double ea, double eb) {
@@ -350,6 +369,8 @@ static void softb_decode(softb_ctx* c, const float* llrs, const double* el, int 
         c->bits[rp] = v;
         c->ebits[lp] = c->hard ? 0.0 : tanh_bound(Lu, u, eLu);
         c->ebits[rp] = c->hard ? 0.0 : tanh_bound(Lv, v, eLv);
+        put_leaf(c->leaf, c->eleaf, lp, Lu, eLu);
+        put_leaf(c->leaf, c->eleaf, rp, Lv, eLv);
         log_sum_avoid_zero_nan(&Lu, &Lv, &top, 1);
         ret[0] = top;
         eret[0] = lse_bound(Lu, Lv, top, eLu, eLv);
@@ -378,7 +399,7 @@ static void softb_decode(softb_ctx* c, const float* llrs, const double* el, int 
 }
 
 void oracle_sc_decode_soft_bound(const float* y, int64_t B, int N, const float* priors, float llr_scale, int hard,
-                                 float* bits_out, double* ebits_out) {
+                                 float* bits_out, double* ebits_out, float* leaf_out, double* eleaf_out) {
     int n = 0;
     while ((1 << n) < N) ++n;
     float zeros[LSE_MAX_N] = {0};
@@ -391,7 +412,8 @@ void oracle_sc_decode_soft_bound(const float* y, int64_t B, int N, const float* 
             llr[i] = llr_scale * y[b * N + i];
             el[i] = 0.0;
         }
-        softb_ctx c = {n, pr, hard, bits_out + b * N, ebits_out + b * N};
+        softb_ctx c = {n, pr, hard, bits_out + b * N, ebits_out + b * N, leaf_out ? leaf_out + b * N : NULL,
+                       eleaf_out ? eleaf_out + b * N : NULL};
         softb_decode(&c, llr, el, 0, 0, ret, eret);
     }
 }

@@ -226,11 +226,11 @@ def gen_lse():
         save(f"lse_{N}_{K}.npz", **out)
 
 
-def gen_lse_soft():
+def gen_lse_soft(cases=None, seed=17):
     """PolarCode.sc_decode_soft (polar.py:281-358), hard and soft decisions, priors None and a random
     prior vector (large priors on frozen positions, as a caller would pass them)."""
-    rng = np.random.default_rng(17)
-    for N, K, per in [(16, 8, 48), (32, 16, 48), (64, 32, 48)]:
+    rng = np.random.default_rng(seed)
+    for N, K, per in cases or [(16, 8, 48), (32, 16, 48), (64, 32, 48)]:
         code = polar_code(N, K)
         torch.manual_seed(5000 + N)
         blocks = []
@@ -259,6 +259,10 @@ def gen_lse_soft():
                 out[f"msg_hat_{tag}"] = np.concatenate(hats)
                 out[f"bits_{tag}"] = np.concatenate(bits)
         save(f"lse_soft_{N}_{K}.npz", **out)
+
+
+def gen_lse_soft_long():
+    gen_lse_soft([(128, 64, 16), (256, 128, 8)], seed=18)
 
 
 def gen_pac():
@@ -407,6 +411,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "pac", "errors", "gru", "gru_wide", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "pac", "errors", "gru", "gru_wide", "conv"]
     for w in which:
         globals()["gen_" + w]()

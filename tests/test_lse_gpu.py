@@ -9,10 +9,11 @@ of g = u a + b, of tanh(L/2) and of the partial-sum products, plus each operatio
 implementations of the model differ by at most 2 E per decoded_bits entry.  Soft partial sums multiply
 LLRs of magnitude ~1e2 (g = u a + b), so E reaches ~1e-2 on ill-conditioned entries -- the drifts up to
 ~0.06 seen before were such entries.  Bars:
-  * hard decisions: >= 99.9 % of information bits and >= 99 % of codewords identical (measured: all);
-    decoded_bits bit-exact on agreeing codewords;
-  * soft decisions: >= 99.5 % of bits and >= 98 % of codewords identical; on agreeing codewords EVERY
-    finite decoded_bits entry within 2 E of the reference (max |diff| / 2E is reported), same NaN positions.
+  * decisions: a decision may differ only where its LLR (the oracle's) is within 2 E_L of zero -- checked
+    for the first disagreement of each codeword in sc_decode (later ones follow from it through the
+    partial sums) and for every disagreement in sc_decode_soft (whose decisions feed nothing);
+  * values: hard decoded_bits bit-exact on agreeing codewords; EVERY finite soft decoded_bits entry within
+    2 E of the reference (max |diff| / 2E is reported), same NaN positions.
 Measured on MI355X (tools/lse_bound_report.py): max |diff| / 2E = 0.125 on every lse_* fixture (the
 oracle-vs-torch figure is the same), max |diff| 1.4e-4 (N = 128).
 """
@@ -37,34 +38,54 @@ def t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-def check(hat, bits, ref_hat, ref_bits, hard, what, E=None):
-    """E: per-entry forward error bound of decoded_bits (required for soft decisions with bits)."""
-    agree = hat == ref_hat
-    bit_bar, row_bar = (0.999, 0.99) if hard else (0.995, 0.98)
-    assert agree.mean() >= bit_bar and agree.all(axis=1).mean() >= row_bar, (what, agree.mean(),
-                                                                               agree.all(axis=1).mean())
+def check(hat, bits, ref_hat, ref_bits, hard, what, bd):
+    """bd = bound(...): the oracle's forward error bounds on the same words.  Decisions: every codeword's
+    first disagreeing information bit (sc_decode: later ones follow from it through the partial sums) --
+    every one for sc_decode_soft, whose decisions feed nothing -- must sit where the decision LLR is
+    within 2 E of zero.  Values: on codewords whose decisions agree (all codewords for sc_decode_soft),
+    hard decoded_bits bit-exact, soft ones within 2 E per entry, same NaN positions."""
+    from oracle import oracle as O
+    bad = O.unexplained_disagreements(hat, ref_hat, bd["info"], bd["leaf"], bd["eleaf"], bd["feedback"])
+    assert not bad, (what, "decision flips the bound does not explain (row, k, L, E)", bad[:5])
     if ref_bits is not None:
-        rows = agree.all(axis=1)  # compare values on codewords whose decisions agree
+        rows = (hat == ref_hat).all(axis=1) if bd["feedback"] else np.ones(hat.shape[0], bool)
         assert np.array_equal(np.isnan(bits[rows]), np.isnan(ref_bits[rows])), what
         fin = ~np.isnan(ref_bits[rows])
         if hard:
-            assert np.array_equal(bits[rows][fin], ref_bits[rows][fin]), what
+            if bd["feedback"]:
+                assert np.array_equal(bits[rows][fin], ref_bits[rows][fin]), what
+            else:  # sign(L): may differ exactly where L is within 2 E of zero (checked above)
+                same = bits[rows][fin] == ref_bits[rows][fin]
+                assert np.all(same | (np.abs(bd["leaf"][rows][fin]) <= 2 * bd["eleaf"][rows][fin])), what
         else:
             err = np.abs(bits[rows][fin].astype(np.float64) - ref_bits[rows][fin])
-            bound = 2.0 * E[rows][fin]
+            bound = 2.0 * bd["E"][rows][fin]
             ratio = err / np.maximum(bound, 1e-300)
             assert np.all(err <= bound), (what, "max |diff| / 2E", float(ratio.max(initial=0.0)),
                                           "max |diff|", float(err.max(initial=0.0)))
 
 
-def lse_bound(y, snr, info):
+def lse_bound(y, snr, info, hard):
     from oracle import oracle as O
-    return O.sc_decode_lse_bound(y, snr, info, False)[1]
+    _, E, leaf, eleaf = O.sc_decode_lse_bound(y, snr, info, hard, leaves=True)
+    return {"E": E, "leaf": leaf, "eleaf": eleaf, "info": np.sort(np.asarray(info)), "feedback": True}
 
 
-def soft_bound(y, snr, prior):
+def soft_bound(y, snr, info, prior, hard):
     from oracle import oracle as O
-    return O.sc_decode_soft_bound(y, snr, False, prior)[1]
+    _, E, leaf, eleaf = O.sc_decode_soft_bound(y, snr, hard, prior, leaves=True)
+    return {"E": E, "leaf": leaf, "eleaf": eleaf, "info": np.sort(np.asarray(info)), "feedback": False}
+
+
+def stack(parts, d):
+    """Per-SNR bound dicts -> one dict in the fixture's row order."""
+    out = {k: np.empty((d["y"].shape[0],) + parts[0][1][k].shape[1:], parts[0][1][k].dtype)
+           for k in ("E", "leaf", "eleaf")}
+    for m, b in parts:
+        for k in out:
+            out[k][m] = b[k]
+    out["info"], out["feedback"] = parts[0][1]["info"], parts[0][1]["feedback"]
+    return out
 
 
 @pytest.mark.parametrize("N,K", LSE_CASES)
@@ -74,13 +95,13 @@ def test_sc_decode_lse_golden(N, K):
     for tag, hard in (("hard", True), ("soft", False)):
         hat = np.empty_like(d[f"msg_hat_{tag}"])
         bits = np.empty_like(d[f"bits_{tag}"])
-        E = np.empty(bits.shape, np.float64)
+        parts = []
         for s in np.unique(d["snr"]):
             m = d["snr"] == s
             h, b = code.sc_decode(t(d["y"][m]), float(s), hard_decision=hard, return_bits=True)
             hat[m], bits[m] = h.cpu().numpy(), b.cpu().numpy()
-            E[m] = lse_bound(d["y"][m], float(s), d["info"])
-        check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag), E)
+            parts.append((m, lse_bound(d["y"][m], float(s), d["info"], hard)))
+        check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag), stack(parts, d))
 
 
 def test_sc_decode_lse_args_default_is_soft():
@@ -111,7 +132,7 @@ def test_sc_decode_lse_vs_oracle_random(oracle, N, K):
         for hard in (True, False):
             h, b = code.sc_decode(t(y), 2.5, hard_decision=hard, return_bits=True)
             oh, ob = oracle.sc_decode_lse(y, 2.5, info, hard)
-            check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), lse_bound(y, 2.5, info))
+            check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), lse_bound(y, 2.5, info, hard))
 
 
 def test_sc_decode_lse_full_size_properties(oracle):
@@ -134,7 +155,7 @@ def test_sc_decode_lse_full_size_properties(oracle):
     for hard in (True, False):
         oh, _ = oracle.sc_decode_lse(ys.cpu().numpy(), 2.0, code.info_positions, hard)
         h = code.sc_decode(ys, 2.0, hard_decision=hard).cpu().numpy()
-        check(h, None, oh, None, hard, hard)
+        check(h, None, oh, None, hard, hard, lse_bound(ys.cpu().numpy(), 2.0, code.info_positions, hard))
 
 
 @pytest.mark.parametrize("N,K", [(8, 4), (32, 16), (64, 32), (128, 64)])
@@ -166,11 +187,11 @@ def test_lse_montecarlo_driver_and_cli(capsys):
 
 
 
-@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32)])
+@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32), (128, 64), (256, 128)])
 def test_sc_decode_soft_golden(N, K):
-    """PolarCode.sc_decode_soft (polar.py:281-358) vs the reference's vectors: with priors the bars of
-    check(); without priors (frozen bits decoded like information bits: leaf 0 is cancellation noise,
-    see test_oracle_golden) >= 99.5 % of bits and >= 98 % of codewords."""
+    """PolarCode.sc_decode_soft (polar.py:281-358) vs the reference's vectors, with the fixture's priors
+    ('pr') and without ('p0': frozen bits are decoded like information bits, so leaf 0's LLR is the
+    boxplus of all N channel LLRs, cancellation-dominated; its sign flips only within the bound)."""
     d = golden(f"lse_soft_{N}_{K}.npz")
     code = polar_for(N, d["info"])
     for hard in (True, False):
@@ -178,24 +199,20 @@ def test_sc_decode_soft_golden(N, K):
             tag = ("hard" if hard else "soft") + "_" + ptag
             hat = np.empty_like(d[f"msg_hat_{tag}"])
             bits = np.empty_like(d[f"bits_{tag}"])
-            E = np.empty(bits.shape, np.float64)
+            parts = []
             for s in np.unique(d["snr"]):
                 m = d["snr"] == s
                 pr = None if ptag == "p0" else d["prior"]
                 h, b = code.sc_decode_soft(t(d["y"][m]), float(s), priors=pr, hard_decision=hard, return_bits=True)
                 hat[m], bits[m] = h.cpu().numpy(), b.cpu().numpy()
-                E[m] = soft_bound(d["y"][m], float(s), pr)
-            if ptag == "pr":
-                check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag), E)
-            else:
-                ag = hat == d[f"msg_hat_{tag}"]
-                assert ag.mean() >= 0.995 and ag.all(axis=1).mean() >= 0.98, (N, tag)
+                parts.append((m, soft_bound(d["y"][m], float(s), d["info"], pr, hard)))
+            check(hat, bits, d[f"msg_hat_{tag}"], d[f"bits_{tag}"], hard, (N, tag), stack(parts, d))
 
 
 def test_sc_decode_soft_vs_oracle_random(oracle):
     """Random words, ragged batches, priors from the frozen set (+20) plus noise, N = 8..64."""
     from neural_polar_decoder_amd.codes import polar_info_positions
-    for N, K in [(8, 4), (32, 16), (64, 32), (64, 22)]:
+    for N, K in [(8, 4), (32, 16), (64, 32), (64, 22), (128, 64), (256, 128)]:
         info = polar_info_positions(N, K)
         code = polar_for(N, info)
         rng = np.random.default_rng(N + 3 * K)
@@ -207,4 +224,4 @@ def test_sc_decode_soft_vs_oracle_random(oracle):
             for hard in (True, False):
                 h, b = code.sc_decode_soft(t(y), 2.5, priors=prior, hard_decision=hard, return_bits=True)
                 oh, ob = oracle.sc_decode_soft(y, 2.5, info, hard, prior)
-                check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), soft_bound(y, 2.5, prior))
+                check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), soft_bound(y, 2.5, info, prior, hard))

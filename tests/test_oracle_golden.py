@@ -179,23 +179,24 @@ def test_sc_decode_lse_golden(oracle, N, K):
         if hard:
             assert np.array_equal(hat, g) and np.array_equal(bits, gb), (N, tag)
         else:
-            assert (hat == g).mean() >= 0.999 and (hat == g).all(axis=1).mean() >= 0.99, (N, tag)
-            E = np.concatenate([oracle.sc_decode_lse_bound(d["y"][d["snr"] == s], float(s), d["info"])[1]
-                                for s in np.unique(d["snr"])])
-            order = np.concatenate([np.nonzero(d["snr"] == s)[0] for s in np.unique(d["snr"])])
-            Eo = np.empty_like(E)
-            Eo[order] = E
-            assert np.array_equal(np.isnan(bits), np.isnan(gb))
-            fin = ~np.isnan(gb)
-            assert np.all(np.abs(bits[fin].astype(np.float64) - gb[fin]) <= 2 * Eo[fin]), (N, tag)
+            for s in np.unique(d["snr"]):
+                m = d["snr"] == s
+                _, E, lf, el = oracle.sc_decode_lse_bound(d["y"][m], float(s), d["info"], leaves=True)
+                assert not oracle.unexplained_disagreements(hat[m], g[m], d["info"], lf, el, True), (N, tag)
+                rows = (hat[m] == g[m]).all(axis=1)
+                b, r = bits[m][rows], gb[m][rows]
+                assert np.array_equal(np.isnan(b), np.isnan(r))
+                fin = ~np.isnan(r)
+                assert np.all(np.abs(b[fin].astype(np.float64) - r[fin]) <= 2 * E[rows][fin]), (N, tag)
 
 
-@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32)])
+@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32), (128, 64), (256, 128)])
 def test_sc_decode_soft_golden(oracle, N, K):
     """PolarCode.sc_decode_soft (polar.py:281-358) with the fixture's priors ('pr': hard decisions
-    bit-exact, soft decoded_bits within 1e-4) and without ('p0': frozen bits are decoded like information
+    bit-exact, soft decoded_bits within 2 E) and without ('p0': frozen bits are decoded like information
     bits, so leaf 0's LLR is the cancellation-dominated boxplus of all N LLRs and its sign is rounding
-    noise of the formula -- >= 99.5 % of bits and >= 98 % of codewords identical)."""
+    noise of the formula -- every disagreement must sit where the leaf LLR is within 2 E of zero; 6 % of
+    the N = 256 fixture's codewords have one)."""
     d = golden(f"lse_soft_{N}_{K}.npz")
     for hard in (True, False):
         for ptag in ("p0", "pr"):
@@ -218,5 +219,8 @@ def test_sc_decode_soft_golden(oracle, N, K):
                         assert np.array_equal(np.isnan(bits[m]), np.isnan(gb[m])), tag
                         fin = ~np.isnan(gb[m])
                         assert np.all(np.abs(bits[m][fin].astype(np.float64) - gb[m][fin]) <= 2 * E[fin]), tag
-            else:
-                assert (hat == g).mean() >= 0.995 and (hat == g).all(axis=1).mean() >= 0.98, tag
+            else:  # decisions differ only where the leaf LLR is within 2 E of zero
+                for s in np.unique(d["snr"]):
+                    m = d["snr"] == s
+                    _, _, lf, el = oracle.sc_decode_soft_bound(d["y"][m], float(s), hard, None, leaves=True)
+                    assert not oracle.unexplained_disagreements(hat[m], g[m], d["info"], lf, el, False), tag
