@@ -244,14 +244,13 @@ def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg):
     from neural_polar_decoder_amd.montecarlo import seeded_crisp
     from neural_polar_decoder_amd.utils import count_errors
     net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev)
-    info = torch.as_tensor(np.asarray(code.info_positions), device=dev)
     c_sc = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     c_gru = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
 
     def step():
         code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc)
         for si in range(len(snrs)):
-            count_errors(msg, dec.decode(net, False, yall[si]).index_select(1, info), c_gru[si])
+            count_errors(msg, dec.decode(net, False, yall[si]), c_gru[si], cols=code.info_positions)
 
     t = timer(step, iters=2, warm=1)
     allreduce(c_gru, _sum(), world)
@@ -326,7 +325,6 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
     from neural_polar_decoder_amd.utils import count_errors
     code = PAC(_ap.Namespace(target_K=64), 128, 64, 91)
     cw0 = rank * B
-    info = torch.as_tensor(np.asarray(code.B), device=dev)
     ys, msg = [], None
     for si, snr in enumerate(snrs):
         m, _, y = code.mc_generate(B, snr, SEED, si, cw0, device=dev, want_msg=msg is None)
@@ -361,7 +359,7 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
 
         def gru_step():
             for si in range(len(snrs)):
-                count_errors(msg, dec.decode(net, False, ys[si]).index_select(1, info), c[si])
+                count_errors(msg, dec.decode(net, False, ys[si]), c[si], cols=code.B)
 
         t = timer(gru_step, iters=1, warm=0)
         ms = event_ms(lambda: dec.decode(net, False, ys[2]), 1, stream)

@@ -185,6 +185,14 @@ int npd_sc_mc_sweep_fused(const npd_code* code, int n_snr, const float* sigma, c
 int npd_count_errors(const float* ref, const float* hat, int64_t B, int K, unsigned long long* counters,
                      void* stream);
 
+/*
+ * As npd_count_errors, comparing ref (B,K) with columns cols[0..K) (HOST array, each < W) of hat (B,W):
+ * the reference's `errors_ber(msg, decoded[:, info])` (rnn_all.py:874-879, run_models.py:333-337)
+ * without materialising the gathered (B,K) copy.  K <= 256.
+ */
+int npd_count_errors_cols(const float* ref, const float* hat, int64_t B, int K, int W, const int32_t* cols,
+                          unsigned long long* counters, void* stream);
+
 /* ---------------------------------------------------------------------------------- CRISP GRU */
 /*
  * Create a GRU decoder from an RNN_Model state dict (rnn_all.py:294-398): nn.GRU(input_size, F,

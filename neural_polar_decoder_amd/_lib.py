@@ -47,6 +47,7 @@ SIGNATURES = [
                                   c_void_p]),
     ("npd_list_prune_select", c_int, [c_void_p, c_int, c_int, c_void_p]),
     ("npd_count_errors", c_int, [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p]),
+    ("npd_count_errors_cols", c_int, [c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("npd_gru_create", c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
     ("npd_gru_destroy", c_int, [c_void_p]),
     ("npd_gru_decode", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),

@@ -199,21 +199,55 @@ __global__ __launch_bounds__(256) void mc_generate_kernel(const CodeParams p, fl
 }
 
 // ---------------------------------------------------------------------------------- error counters
-__global__ __launch_bounds__(256) void count_errors_kernel(const float* __restrict__ ref, const float* __restrict__ hat,
-                                                           int64_t B, int K, unsigned long long* counters) {
+// One wave per row at a time, lanes over the K compared positions: the reference row and the decision
+// row are read with consecutive-lane (coalesced) loads, a ballot + popcount counts the row's bit errors,
+// and a nonzero count is a block error.  Four rows are in flight per wave iteration.  Decisions may be
+// full (B, W) rows read at columns cols[k] (e.g. decoded (B, N) at the information positions) so no
+// gathered (B, K) copy is made.  One counter atomic pair per workgroup.
+struct CountArgs {
+    const float* ref;
+    const float* hat;
+    unsigned long long* counters;
+    int64_t B;
+    int K, W, use_cols;
+    int32_t cols[kMaxN];
+};
+
+__global__ __launch_bounds__(256) void count_errors_kernel(const CountArgs a) {
+    __shared__ uint32_t red[2];
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 2) red[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t nw = (int64_t)gridDim.x * 4;
     uint32_t eb = 0, bl = 0;
-    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < B; b += (int64_t)gridDim.x * blockDim.x) {
-        uint32_t e = 0;
-        for (int k = 0; k < K; ++k) e += (rintf(ref[b * K + k]) != rintf(hat[b * K + k])) ? 1u : 0u;
-        eb += e;
-        bl += e ? 1u : 0u;
+    for (int64_t r0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r0 < a.B; r0 += 4 * nw) {
+        uint32_t ne[4] = {0u, 0u, 0u, 0u};
+        for (int k0 = 0; k0 < a.K; k0 += 64) {
+            const int k = k0 + lane;
+            const int c = k < a.K ? (a.use_cols ? a.cols[k] : k) : 0;
+            float rv[4], hv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t r = r0 + u * nw;
+                const bool ok = k < a.K && r < a.B;
+                rv[u] = ok ? a.ref[r * a.K + k] : 0.0f;
+                hv[u] = ok ? a.hat[r * a.W + c] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ne[u] += (uint32_t)__builtin_popcountll(__ballot(rintf(rv[u]) != rintf(hv[u])));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            eb += ne[u];
+            bl += ne[u] ? 1u : 0u;
+        }
     }
-    eb = wave_sum_u32(eb);
-    bl = wave_sum_u32(bl);
-    if ((threadIdx.x & 63) == 0 && (eb | bl)) {
-        atomicAdd(counters + 0, (unsigned long long)eb);
-        atomicAdd(counters + 1, (unsigned long long)bl);
+    if (lane == 0 && (eb | bl)) {
+        atomicAdd(&red[0], eb);
+        atomicAdd(&red[1], bl);
     }
+    __syncthreads();
+    if (threadIdx.x < 2 && red[threadIdx.x]) atomicAdd(a.counters + threadIdx.x, (unsigned long long)red[threadIdx.x]);
 }
 
 }  // namespace gen
@@ -284,13 +318,48 @@ extern "C" int npd_mc_generate(const npd_code* code, float* msg, float* x, float
     }
 }
 
+static int count_launch(gen::CountArgs& a, hipStream_t s) {
+    const int64_t groups = (a.B + 15) / 16;  // 4 waves x 4 rows in flight
+    const int grid = grid_for(groups, 8, device_cu_count());
+    hipLaunchKernelGGL(gen::count_errors_kernel, dim3(grid), dim3(256), 0, s, a);
+    return launch_check("count_errors_kernel launch");
+}
+
 extern "C" int npd_count_errors(const float* ref, const float* hat, int64_t B, int K, unsigned long long* counters,
                                 void* stream) {
     NPD_ARG(B >= 0 && K >= 0, "npd_count_errors: negative size");
     NPD_ARG(counters != nullptr, "npd_count_errors: counters is NULL");
     if (B == 0 || K == 0) return NPD_OK;
     NPD_ARG(ref != nullptr && hat != nullptr, "npd_count_errors: null pointer");
-    const int grid = grid_for((B + 255) / 256, 8, device_cu_count());
-    hipLaunchKernelGGL(gen::count_errors_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ref, hat, B, K, counters);
-    return launch_check("count_errors_kernel launch");
+    gen::CountArgs a{};
+    a.ref = ref;
+    a.hat = hat;
+    a.counters = counters;
+    a.B = B;
+    a.K = K;
+    a.W = K;
+    a.use_cols = 0;
+    return count_launch(a, (hipStream_t)stream);
+}
+
+extern "C" int npd_count_errors_cols(const float* ref, const float* hat, int64_t B, int K, int W, const int32_t* cols,
+                                     unsigned long long* counters, void* stream) {
+    NPD_ARG(B >= 0 && K >= 0 && W >= 0, "npd_count_errors_cols: negative size");
+    NPD_ARG(counters != nullptr && cols != nullptr, "npd_count_errors_cols: NULL counters / cols");
+    NPD_ARG(K <= kMaxN, "npd_count_errors_cols: K <= 256");
+    if (B == 0 || K == 0) return NPD_OK;
+    NPD_ARG(ref != nullptr && hat != nullptr, "npd_count_errors_cols: null pointer");
+    gen::CountArgs a{};
+    for (int k = 0; k < K; ++k) {
+        NPD_ARG(cols[k] >= 0 && cols[k] < W, "npd_count_errors_cols: column out of range");
+        a.cols[k] = cols[k];
+    }
+    a.ref = ref;
+    a.hat = hat;
+    a.counters = counters;
+    a.B = B;
+    a.K = K;
+    a.W = W;
+    a.use_cols = 1;
+    return count_launch(a, (hipStream_t)stream);
 }

@@ -186,13 +186,14 @@ class DecoderMonteCarlo(MonteCarlo):
     def decisions(self, y):  # pragma: no cover - abstract
         raise NotImplementedError
 
-    def count(self, msg, hat, counters_row):
+    def count(self, msg, dec, counters_row):
+        """msg (n,K) vs the decisions' information columns dec[:, info] (n,N), not gathered."""
         from .utils import count_errors
-        count_errors(msg, hat, counters_row)
+        count_errors(msg, dec, counters_row, cols=self.info_np)
 
     def count_batch(self, si, snr, cw_offset, n, counters_row):
         msg, y = self.generate(si, snr, cw_offset, n)
-        self.count(msg, self.decisions(y).index_select(1, self.info), counters_row)
+        self.count(msg, self.decisions(y), counters_row)
 
 
 class GRUMonteCarlo(DecoderMonteCarlo):

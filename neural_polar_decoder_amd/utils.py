@@ -28,21 +28,31 @@ def sigma_f32(snr) -> float:
     return float(np.float32(snr_db2sigma(snr)))
 
 
-def count_errors(y_true: torch.Tensor, y_pred: torch.Tensor, counters: torch.Tensor | None = None) -> torch.Tensor:
+def count_errors(y_true: torch.Tensor, y_pred: torch.Tensor, counters: torch.Tensor | None = None,
+                 cols=None) -> torch.Tensor:
     """Device counters [bit errors, block errors] (uint64 stored in an int64 tensor), accumulated.
 
-    Host inputs are staged to the GPU of ``counters`` (or the current HIP device)."""
+    ``cols`` (K ints): compare y_true (B,K) with y_pred[:, cols] of a (B,W) y_pred without gathering it
+    (npd_count_errors_cols).  Host inputs are staged to the GPU of ``counters`` (or the current device)."""
     dev = counters.device if counters is not None and counters.is_cuda else None
     t = _lib.stage(y_true, "y_true", dev)
     p = _lib.stage(y_pred, "y_pred", t.device)
     t = _lib.f32c(t.reshape(t.shape[0], -1))
     p = _lib.f32c(p.reshape(p.shape[0], -1))
-    if t.shape != p.shape:
-        raise ValueError(f"shape mismatch {tuple(t.shape)} vs {tuple(p.shape)}")
     if counters is None:
         counters = torch.zeros(2, dtype=torch.int64, device=t.device)
     _lib.require_gpu(counters, "counters")
     L = _lib.load()
+    if cols is not None:
+        c = np.ascontiguousarray(np.asarray(cols, dtype=np.int64).reshape(-1), dtype=np.int32)
+        if t.shape[0] != p.shape[0] or c.size != t.shape[1]:
+            raise ValueError(f"shape mismatch {tuple(t.shape)} vs {tuple(p.shape)} at {c.size} columns")
+        _lib.check(L.npd_count_errors_cols(_lib.ptr(t), _lib.ptr(p), t.shape[0], t.shape[1], p.shape[1],
+                                           c.ctypes.data_as(_lib.c_void_p), _lib.ptr(counters),
+                                           _lib.stream_of(t.device)), "npd_count_errors_cols")
+        return counters
+    if t.shape != p.shape:
+        raise ValueError(f"shape mismatch {tuple(t.shape)} vs {tuple(p.shape)}")
     _lib.check(L.npd_count_errors(_lib.ptr(t), _lib.ptr(p), t.shape[0], t.shape[1], _lib.ptr(counters),
                                   _lib.stream_of(t.device)), "npd_count_errors")
     return counters

@@ -127,8 +127,8 @@ def _oracle_decoder_mc(kind, rank=None, world=None):
         def decisions(self, y):
             return torch.from_numpy(np.ascontiguousarray(decide(y.numpy()), dtype=np.float32))
 
-        def count(self, msg, hat, row):
-            be, bl = O.count_errors(msg.numpy(), np.ascontiguousarray(hat.numpy()))
+        def count(self, msg, dec, row):
+            be, bl = O.count_errors(msg.numpy(), np.ascontiguousarray(dec.numpy()[:, self.info_np]))
             row[0] += be
             row[1] += bl
 

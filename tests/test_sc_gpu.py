@@ -359,3 +359,17 @@ def test_montecarlo_fused_equals_unfused():
     a = SCMonteCarlo(code, [0.0, 2.0, 4.0], 70_001, 30_000, seed=3).run()
     b = SCMonteCarlo(code, [0.0, 2.0, 4.0], 70_001, 30_000, seed=3, fused=False).run()
     assert a.bit_errors == b.bit_errors and a.block_errors == b.block_errors
+
+
+def test_count_errors_cols_equals_gather(oracle):
+    """npd_count_errors_cols (decisions read at the information columns of the full (B,N) rows) ==
+    npd_count_errors on the gathered (B,K) copy == the oracle; zeros count as errors."""
+    from neural_polar_decoder_amd.utils import count_errors
+    rng = np.random.default_rng(4)
+    for B, N, K in [(100_003, 64, 32), (777, 256, 200), (5, 16, 1)]:
+        info = np.sort(rng.choice(N, K, replace=False))
+        dec = rng.choice(np.array([-1.0, 0.0, 1.0], np.float32), size=(B, N), p=[0.45, 0.1, 0.45])
+        msg = (1 - 2 * (rng.random((B, K)) < 0.5)).astype(np.float32)
+        c1 = count_errors(t(msg), t(dec), cols=info)
+        c2 = count_errors(t(msg), t(np.ascontiguousarray(dec[:, info])))
+        assert c1.cpu().tolist() == c2.cpu().tolist() == list(oracle.count_errors(msg, np.ascontiguousarray(dec[:, info])))
