@@ -137,8 +137,17 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
     }
 }
 
+// Waves per workgroup of the F <= 64 kernels: all share the workgroup's LDS copy of the weights; 8 waves
+// put two on every SIMD, so one wave's gate nonlinearities (VALU) overlap the other's MFMAs.
+#ifndef NPD_GRU_WPB
+#define NPD_GRU_WPB 8
+#endif
+#ifndef NPD_GRU_BF_WPB
+#define NPD_GRU_BF_WPB 4
+#endif
+
 template <int F, int L>
-__global__ __launch_bounds__(256) void gru_decode_kernel(const Args a) {
+__global__ __launch_bounds__(64 * NPD_GRU_WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
     extern __shared__ __attribute__((aligned(16))) f4 smem4[];
@@ -156,7 +165,8 @@ __global__ __launch_bounds__(256) void gru_decode_kernel(const Args a) {
     const int64_t ntiles = (a.B + 31) / 32;
     const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU_WPB + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * NPD_GRU_WPB) {
         const int64_t cw = tile * 32 + col;
         const bool valid = cw < a.B;
         const int64_t cwc = valid ? cw : a.B - 1;
@@ -349,9 +359,9 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
         attr = true;
     }
     const int64_t tiles = (a.B + 31) / 32;
-    const int64_t wgs = (tiles + 3) / 4;
+    const int64_t wgs = (tiles + NPD_GRU_WPB - 1) / NPD_GRU_WPB;
     const int grid = grid_for(wgs, 1, device_cu_count());
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU_WPB), lds, s, a);
     (void)g;
     return launch_check("gru_decode_kernel launch");
 }
@@ -450,7 +460,7 @@ __device__ __forceinline__ void gemm_bf(const f4* __restrict__ smem4, int g, int
 }
 
 template <int F, int L, int SPLIT>
-__global__ __launch_bounds__(256) void gru_decode_bf_kernel(const ArgsB a) {
+__global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(const ArgsB a) {
     using G = GeoB<F, L, SPLIT>;
     constexpr int TT = G::TT, HT = G::HT, KB = G::KB, IMG = G::IMG;
     extern __shared__ __attribute__((aligned(16))) f4 smem4[];
@@ -469,7 +479,8 @@ __global__ __launch_bounds__(256) void gru_decode_bf_kernel(const ArgsB a) {
     const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float one_or_zero = half ? 0.0f : 1.0f;
 
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU_BF_WPB + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * NPD_GRU_BF_WPB) {
         const int64_t cw = tile * 32 + col;
         const bool valid = cw < a.B;
         const int64_t cwc = valid ? cw : a.B - 1;
@@ -659,9 +670,9 @@ static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
         attr = true;
     }
     const int64_t tiles = (a.B + 31) / 32;
-    const int64_t wgs = (tiles + 3) / 4;
+    const int64_t wgs = (tiles + NPD_GRU_BF_WPB - 1) / NPD_GRU_BF_WPB;
     const int grid = grid_for(wgs, 1, device_cu_count());
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU_BF_WPB), lds, s, a);
     (void)g;
     return launch_check("gru_decode_bf_kernel launch");
 }

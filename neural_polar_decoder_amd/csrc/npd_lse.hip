@@ -482,6 +482,10 @@ extern "C" int npd_sc_decode_soft(const npd_code* code, const float* y, float ll
     a.B = B;
     a.scale = llr_scale;
     for (int i = 0; i < kMaxN; ++i) a.prior[i] = (priors && i < code->p.N) ? priors[i] : 0.0f;
+    if (getenv("NPD_SOFT_LDS")) {  // force the LDS-resident variant (testing / A-B)
+        return hard_decision ? lse::launch_soft_lds<false>(code->p, a, (hipStream_t)stream)
+                             : lse::launch_soft_lds<true>(code->p, a, (hipStream_t)stream);
+    }
     return hard_decision ? lse::dispatch_soft<false>(code->p, a, (hipStream_t)stream)
                          : lse::dispatch_soft<true>(code->p, a, (hipStream_t)stream);
 }

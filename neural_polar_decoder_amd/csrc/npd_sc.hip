@@ -110,6 +110,7 @@ struct Ctx {
     uint32_t lvl_row[9];  // per-level LDS rows for upper levels (node size > R, < N)
     float scale;
     uint32_t flags;
+    int64_t next_row0;    // N > R: the next tile's first row (prefetched after the root g-step), or -1
 };
 
 template <int N>
@@ -246,6 +247,26 @@ __device__ __forceinline__ void up_put(Ctx<N, R, PAC, FULL>& c, int j, float v) 
     else lds_wr(c.lds, c.lvl_row[D] + 4 * j, v);
 }
 
+// ------------------------------------------------------------------------------ tile staging
+// the 64 x N fp32 y tile starting at row0 -> LDS staging buffer: C x 1 KiB global_load_lds (asynchronous;
+// consumers wait with s_waitcnt vmcnt(0)), swizzled source addresses
+template <int N>
+__device__ __forceinline__ void stage_tile(char* lds, const Args& a, int64_t row0, int lane) {
+    constexpr int C = N / 4;
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        const int pch = k * kWave + lane;
+        const int r = pch / C;
+        const int q = pch % C;
+        const int cc = q ^ swz<C>(r);
+        int64_t grow = row0 + r;
+        if (grow >= a.B) grow = a.B - 1;
+        const float* src = a.y + grow * N + cc * 4;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(lds + a.off_stage + k * 1024), 16, 0, 0);
+    }
+}
+
 template <int N, int R, bool PAC, bool FULL, int D, int S0>
 __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a) {
     if constexpr ((1 << D) == R) {
@@ -283,6 +304,12 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
                     up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + e,
                                              g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
                 }
+            }
+            // the staged tile's last read: prefetch the next tile into the buffer while the right half of
+            // this one is decoded (the reads above must complete before the DMA overwrites the buffer)
+            if (c.next_row0 >= 0) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                stage_tile<N>(c.lds, a, c.next_row0, (int)threadIdx.x);
             }
         } else {
 #pragma unroll
@@ -374,23 +401,14 @@ __global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kern
     uint32_t err_bits = 0, err_blocks = 0;
     const bool count = (a.flags & kCount) != 0;
 
+    bool staged = false;
     for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
 
-        // ---- stage the y tile: C x 1 KiB global_load_lds, swizzled source addresses
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            const int pch = k * kWave + lane;
-            const int r = pch / C;
-            const int q = pch % C;
-            const int cc = q ^ swz<C>(r);
-            int64_t grow = row0 + r;
-            if (grow >= a.B) grow = a.B - 1;
-            const float* src = a.y + grow * N + cc * 4;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(lds + a.off_stage + k * 1024), 16, 0, 0);
-        }
+        // ---- stage the y tile (N > R: already in flight since the previous tile's root g-step)
+        if (!staged) stage_tile<N>(lds, a, row0, lane);
+        c.next_row0 = (R < N && t + gridDim.x < a.ntiles) ? (t + gridDim.x) * kWave : -1;
         if constexpr (FULL && R < N) {
             int64_t grow = row0 + lane;
             if (grow >= a.B) grow = a.B - 1;
@@ -426,6 +444,7 @@ __global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kern
         } else {
             node_up<N, R, PAC, FULL, n, 0>(c, p, a);
         }
+        staged = c.next_row0 >= 0;
 
         // ---- error counting against the Philox message stream (utils.py:17-51 semantics)
         if (count) {

@@ -155,3 +155,30 @@ def test_rnn_from_checkpoint_f512(tmp_path):
     info = d["info"]
     assert (out[:, info] == d["decoded"][:, info]).mean() >= 0.999
     assert (out == d["decoded"]).all(1).mean() >= 0.99
+
+
+def test_montecarlo_cli_crisp_and_conv(capsys):
+    """montecarlo CLI with the neural decoders (seeded weights): the reference's output lines appear and
+    the GRU / conv counts equal a direct decode of the same Philox words."""
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import _main, seeded_conv, seeded_crisp
+    from neural_polar_decoder_amd.utils import count_errors
+    _main(["--N", "64", "--K", "32", "--test_size", "3000", "--batch_size", "1024", "--snr_points", "2",
+           "--crisp", "--rnn_feature_size", "32", "--conv", "--embed_dim", "16", "--seed", "9"])
+    out = capsys.readouterr().out
+    assert "BERs of RNN" in out and "BERs of Xformer" in out and "BERs of SC decoding" in out
+    import json
+    rec = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    code = reference_polar_code(64, 32)
+    net, dec = seeded_crisp(code, 32, 2, seed=0, device=DEV)
+    cnet = seeded_conv(64, 16, seed=0, device=DEV)
+    for si, snr in enumerate(rec["crisp_gru"]["snr"]):
+        cg = torch.zeros(2, dtype=torch.int64, device=DEV)
+        cc = torch.zeros(2, dtype=torch.int64, device=DEV)
+        for off in range(0, 3000, 1024):
+            n = min(1024, 3000 - off)
+            msg, _, y = code.mc_generate(n, snr, 9, si, off, device=DEV)
+            count_errors(msg, dec.decode(net, False, y), cg, cols=code.info_positions)
+            count_errors(msg, cnet.logits(y)[1], cc, cols=code.info_positions)
+        assert cg[0].item() == rec["crisp_gru"]["bit_errors"][si] and cg[1].item() == rec["crisp_gru"]["block_errors"][si]
+        assert cc[0].item() == rec["conv"]["bit_errors"][si] and cc[1].item() == rec["conv"]["block_errors"][si]

@@ -13,7 +13,9 @@ LLRs of magnitude ~1e2 (g = u a + b), so E reaches ~1e-2 on ill-conditioned entr
     for the first disagreement of each codeword in sc_decode (later ones follow from it through the
     partial sums) and for every disagreement in sc_decode_soft (whose decisions feed nothing);
   * values: hard decoded_bits bit-exact on agreeing codewords; EVERY finite soft decoded_bits entry within
-    2 E of the reference (max |diff| / 2E is reported), same NaN positions.
+    2 E of the reference (max |diff| / 2E is reported); same NaN positions wherever the leaf's bound is
+    finite (a leaf whose computation met an inf/NaN -- crafted words whose LLRs approach exp's overflow --
+    may be finite in one implementation and NaN in the other: an ulp decides whether exp overflows).
 Measured on MI355X (tools/lse_bound_report.py): max |diff| / 2E = 0.125 on every lse_* fixture (the
 oracle-vs-torch figure is the same), max |diff| 1.4e-4 (N = 128).
 """
@@ -49,8 +51,11 @@ def check(hat, bits, ref_hat, ref_bits, hard, what, bd):
     assert not bad, (what, "decision flips the bound does not explain (row, k, L, E)", bad[:5])
     if ref_bits is not None:
         rows = (hat == ref_hat).all(axis=1) if bd["feedback"] else np.ones(hat.shape[0], bool)
-        assert np.array_equal(np.isnan(bits[rows]), np.isnan(ref_bits[rows])), what
-        fin = ~np.isnan(ref_bits[rows])
+        # finiteness may differ only at leaves whose computation met an inf/NaN (the bound is then not
+        # finite): there an ulp of difference decides whether exp overflows (crafted |LLR| >> 1 words)
+        nb, nr = np.isnan(bits[rows]), np.isnan(ref_bits[rows])
+        assert np.all((nb == nr) | ~np.isfinite(bd["eleaf"][rows])), what
+        fin = ~nb & ~nr
         if hard:
             if bd["feedback"]:
                 assert np.array_equal(bits[rows][fin], ref_bits[rows][fin]), what
