@@ -14,6 +14,7 @@
 // projection, W_ih0[:, :N] y, is constant over the N steps and computed once per codeword (P); the
 // one-hot / previous-decision column and all biases are folded into one extra MFMA k-step whose B
 // operand is [1, x_i].
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -137,17 +138,19 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
     }
 }
 
-// Waves per workgroup of the F <= 64 kernels: all share the workgroup's LDS copy of the weights; 8 waves
-// put two on every SIMD, so one wave's gate nonlinearities (VALU) overlap the other's MFMAs.
+// Waves per workgroup of the F <= 64 kernels: all share the workgroup's LDS copy of the weights.  8 waves
+// would put two on every SIMD (one wave's gate VALU work overlapping the other's MFMAs), but at <= 256
+// registers per wave the F = 64, 2-layer kernel spills (P, both states, the gate accumulators and the
+// weight look-ahead need ~300): measured 0.63 of the fp32 MFMA peak vs 0.77 with 4 waves.
 #ifndef NPD_GRU_WPB
-#define NPD_GRU_WPB 8
+#define NPD_GRU_WPB 4   // default (measured: 8 waves spill 716 B/lane and run 0.63 vs 0.77 of peak); NPD_GRU_WAVES=8 A/B
 #endif
 #ifndef NPD_GRU_BF_WPB
 #define NPD_GRU_BF_WPB 4
 #endif
 
-template <int F, int L>
-__global__ __launch_bounds__(64 * NPD_GRU_WPB) void gru_decode_kernel(const Args a) {
+template <int F, int L, int WPB>
+__global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
     extern __shared__ __attribute__((aligned(16))) f4 smem4[];
@@ -165,8 +168,7 @@ __global__ __launch_bounds__(64 * NPD_GRU_WPB) void gru_decode_kernel(const Args
     const int64_t ntiles = (a.B + 31) / 32;
     const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU_WPB + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * NPD_GRU_WPB) {
+    for (int64_t tile = (int64_t)blockIdx.x * WPB + wave; tile < ntiles; tile += (int64_t)gridDim.x * WPB) {
         const int64_t cw = tile * 32 + col;
         const bool valid = cw < a.B;
         const int64_t cwc = valid ? cw : a.B - 1;
@@ -348,10 +350,10 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L>
-static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
+template <int F, int L, int WPB>
+static int launch_w(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
-    auto kern = gru_decode_kernel<F, L>;
+    auto kern = gru_decode_kernel<F, L, WPB>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -359,11 +361,25 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
         attr = true;
     }
     const int64_t tiles = (a.B + 31) / 32;
-    const int64_t wgs = (tiles + NPD_GRU_WPB - 1) / NPD_GRU_WPB;
+    const int64_t wgs = (tiles + WPB - 1) / WPB;
     const int grid = grid_for(wgs, 1, device_cu_count());
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU_WPB), lds, s, a);
-    (void)g;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WPB), lds, s, a);
     return launch_check("gru_decode_kernel launch");
+}
+
+static int gru_waves() {
+    static int w = -1;
+    if (w < 0) {
+        const char* e = getenv("NPD_GRU_WAVES");
+        w = (e && atoi(e) == 4) ? 4 : (e && atoi(e) == 8) ? 8 : NPD_GRU_WPB;
+    }
+    return w;
+}
+
+template <int F, int L>
+static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
+    (void)g;
+    return gru_waves() == 4 ? launch_w<F, L, 4>(a, s) : launch_w<F, L, 8>(a, s);
 }
 
 

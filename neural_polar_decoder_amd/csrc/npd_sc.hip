@@ -110,7 +110,7 @@ struct Ctx {
     uint32_t lvl_row[9];  // per-level LDS rows for upper levels (node size > R, < N)
     float scale;
     uint32_t flags;
-    int64_t next_row0;    // N > R: the next tile's first row (prefetched after the root g-step), or -1
+    const float4* yrow;   // N > R: this lane's received word in HBM (the root level is read from it directly)
 };
 
 template <int N>
@@ -275,11 +275,11 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
     } else {
         constexpr int h = 1 << (D - 1);
         if constexpr ((1 << D) == N) {
-            // read the staging row chunk-wise (4 values of a and of b per pair of ds_read_b128)
+            // the root level straight from this lane's row in HBM (16-B loads)
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 A = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q);
-                const float4 Bv = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q + h / 4);
+                const float4 A = c.yrow[q];
+                const float4 Bv = c.yrow[q + h / 4];
                 up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 0, f_minsum(rmul(c.scale, A.x), rmul(c.scale, Bv.x)));
                 up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 1, f_minsum(rmul(c.scale, A.y), rmul(c.scale, Bv.y)));
                 up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 2, f_minsum(rmul(c.scale, A.z), rmul(c.scale, Bv.z)));
@@ -294,8 +294,8 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
         if constexpr ((1 << D) == N) {
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 A = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q);
-                const float4 Bv = stage_chunk<N>(c.lds, a.off_stage, c.stage_row, c.sw, q + h / 4);
+                const float4 A = c.yrow[q];  // second read of the row: L2 / MALL
+                const float4 Bv = c.yrow[q + h / 4];
                 const float av[4] = {A.x, A.y, A.z, A.w};
                 const float bv[4] = {Bv.x, Bv.y, Bv.z, Bv.w};
 #pragma unroll
@@ -304,12 +304,6 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
                     up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + e,
                                              g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
                 }
-            }
-            // the staged tile's last read: prefetch the next tile into the buffer while the right half of
-            // this one is decoded (the reads above must complete before the DMA overwrites the buffer)
-            if (c.next_row0 >= 0) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                stage_tile<N>(c.lds, a, c.next_row0, (int)threadIdx.x);
             }
         } else {
 #pragma unroll
@@ -401,14 +395,19 @@ __global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kern
     uint32_t err_bits = 0, err_blocks = 0;
     const bool count = (a.flags & kCount) != 0;
 
-    bool staged = false;
     for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
 
-        // ---- stage the y tile (N > R: already in flight since the previous tile's root g-step)
-        if (!staged) stage_tile<N>(lds, a, row0, lane);
-        c.next_row0 = (R < N && t + gridDim.x < a.ntiles) ? (t + gridDim.x) * kWave : -1;
+        // ---- N <= R: stage the y tile through LDS (coalesced, transposed to row-per-lane).  N > R: each
+        // lane reads the root level of its own row straight from HBM at the root's f and g steps (no LDS
+        // stage: the LDS then holds only decision rows, so occupancy is register-bound)
+        if constexpr (R == N) {
+            stage_tile<N>(lds, a, row0, lane);
+        } else {
+            const int64_t grow = (row0 + lane) < a.B ? row0 + lane : a.B - 1;
+            c.yrow = reinterpret_cast<const float4*>(a.y + grow * N);
+        }
         if constexpr (FULL && R < N) {
             int64_t grow = row0 + lane;
             if (grow >= a.B) grow = a.B - 1;
@@ -444,7 +443,6 @@ __global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kern
         } else {
             node_up<N, R, PAC, FULL, n, 0>(c, p, a);
         }
-        staged = c.next_row0 >= 0;
 
         // ---- error counting against the Philox message stream (utils.py:17-51 semantics)
         if (count) {
@@ -533,7 +531,7 @@ static Layout make_layout(bool pac, uint32_t flags) {
         L.off_gt = (flags & kGt) ? off : 0;
         if (flags & kGt) off = align16(off + frow);
     } else {
-        off = align16(stage);
+        off = 0;         // no y stage: the root level is read from HBM per lane
         L.off_leaf = 0;  // leaf LLRs and genie rows go straight to/from HBM
         L.off_gt = 0;
     }
@@ -625,6 +623,7 @@ extern "C" int npd_sc_decode(const npd_code* code, const float* y, float llr_sca
     NPD_ARG(B >= 0, "npd_sc_decode: B < 0");
     NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode: y is NULL");
     NPD_ARG(code->p.pac || u_hat == nullptr, "npd_sc_decode: u_hat is only produced for PAC codes");
+    NPD_ARG((((uintptr_t)y) & 15) == 0, "npd_sc_decode: y must be 16-byte aligned");
     sc::Args a{};
     a.y = y;
     a.leaf = leaf_llr;
@@ -645,6 +644,7 @@ extern "C" int npd_sc_decode_mc(const npd_code* code, const float* y, float llr_
     NPD_ARG(B >= 0, "npd_sc_decode_mc: B < 0");
     NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_mc: y is NULL");
     NPD_ARG(counters != nullptr, "npd_sc_decode_mc: counters is NULL");
+    NPD_ARG((((uintptr_t)y) & 15) == 0, "npd_sc_decode_mc: y must be 16-byte aligned");
     sc::Args a{};
     a.y = y;
     a.msg = msg_hat;

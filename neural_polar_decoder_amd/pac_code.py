@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .codes import pac_info_positions
-from .polar import _CodeHandle, _Philox
+from .polar import _aligned, _CodeHandle, _Philox
 from .utils import llr_scale, sigma_f32
 
 
@@ -116,7 +116,7 @@ class PAC:
 
     # ------------------------------------------------------------------ SC (pac_code.py:534-573)
     def pac_sc_decode(self, corrupted_codewords, snr, use_gt_codeword=None):
-        y = _lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords"))
+        y = _aligned(_lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords")))
         Bn = y.shape[0]
         h = self._code_for(self.B)
         llr = torch.empty(Bn, self.N, dtype=torch.float32, device=y.device)
@@ -147,6 +147,7 @@ class PAC:
 
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
+        y = _aligned(_lib.f32c(y))
         h = self._code_for(self.B)
         _lib.check(_lib.load().npd_sc_decode_mc(h.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(msg_hat), int(seed),
                                                 int(cw_offset), y.shape[0], _lib.ptr(counters), _lib.stream_of(y.device)),

@@ -152,7 +152,7 @@ class PolarCode:
     # ------------------------------------------------------------------ SC (polar.py:465-484)
     def sc_decode_new(self, corrupted_codewords, snr, use_gt=None):
         """Min-sum SC; returns (leaf LLRs incl. the frozen prior (B,N), msg_hat (B,K)) bit-exactly."""
-        y = _lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords"))
+        y = _aligned(_lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords")))
         B = y.shape[0]
         leaf = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
         hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
@@ -163,7 +163,7 @@ class PolarCode:
 
     def sc_decode_msg(self, corrupted_codewords, snr):
         """msg_hat only (no leaf LLR traffic): the form the BER/BLER loops consume."""
-        y = _lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords"))
+        y = _aligned(_lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords")))
         hat = torch.empty(y.shape[0], self.K, dtype=torch.float32, device=y.device)
         _lib.check(_lib.load().npd_sc_decode(self.code.h, _lib.ptr(y), llr_scale(snr), None, _lib.ptr(hat), None, None,
                                              y.shape[0], _lib.stream_of(y.device)), "npd_sc_decode")
@@ -265,7 +265,7 @@ class PolarCode:
         scales = np.asarray([llr_scale(s) for s in snrs], dtype=np.float32)
         if len(scales) != n:
             raise ValueError("one SNR per y segment")
-        y = _lib.f32c(y)
+        y = _aligned(_lib.f32c(y))
         _lib.check(_lib.load().npd_sc_decode_mc_sweep(self.code.h, n, _lib.ptr(y), scales.ctypes.data_as(ctypes.c_void_p),
                                                       _lib.ptr(msg_hat), int(seed), int(cw_offset), B,
                                                       _lib.ptr(counters), _lib.stream_of(y.device)),
@@ -287,6 +287,7 @@ class PolarCode:
 
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
+        y = _aligned(_lib.f32c(y))
         _lib.check(_lib.load().npd_sc_decode_mc(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(msg_hat), int(seed),
                                                 int(cw_offset), y.shape[0], _lib.ptr(counters), _lib.stream_of(y.device)),
                    "npd_sc_decode_mc")
