@@ -472,9 +472,11 @@ __device__ __forceinline__ void gen_llrs(float* lv, const uint32_t (&U)[(N + 31)
     }
 }
 
+// GEN (nothing staged, ~108 VGPRs): two 8-wave workgroups per CU = 4 waves per SIMD hide the Philox /
+// Box-Muller dependency chains; the streaming decoder keeps one workgroup (LDS-bound, 2 waves per SIMD)
 template <int N, uint64_t MASK = 0, bool SPEC = false, bool GEN = false>
-__global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) void sc_fast_kernel(const CodeParams p,
-                                                                                                   const Args a) {
+__global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_SCF_WPB) void sc_fast_kernel(
+    const CodeParams p, const Args a) {
     constexpr int KC = N - __builtin_popcountll(MASK);  // information bits of a specialised code
     extern __shared__ __attribute__((aligned(16))) char lds_all[];
     constexpr int n = log2c<N>();
@@ -485,10 +487,11 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, NPD_SCF_WPE * 4 / NPD_SCF_WPB) vo
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
     const int lane = threadIdx.x & 63;
     // per-wave LDS: the staged tile (64 rows x N fp32) then 64 decision rows of NB bytes
-    const uint32_t per_wave = (uint32_t)(kWave * N * 4 + kWave * NB);
+    constexpr uint32_t kStageBytes = GEN ? 0u : (uint32_t)(kWave * N * 4);  // GEN generates y in registers
+    const uint32_t per_wave = kStageBytes + (uint32_t)(kWave * NB);
     char* lds = lds_all + wave * per_wave;
     constexpr uint32_t kStage = 0;
-    constexpr uint32_t kU = (uint32_t)(kWave * N * 4);
+    constexpr uint32_t kU = kStageBytes;
 
     Lane<N> c;
     c.lds = lds;
@@ -717,7 +720,7 @@ template <int N, uint64_t MASK = 0, bool SPEC = false, bool GEN = false>
 static int launch(const CodeParams& p, Args a, hipStream_t s) {
     constexpr int KC = N - __builtin_popcountll(MASK);
     const int NB = row_stride(SPEC ? KC : p.K);
-    const size_t per_wave = (size_t)kWave * N * 4 + (size_t)kWave * NB;
+    const size_t per_wave = (GEN ? (size_t)0 : (size_t)kWave * N * 4) + (size_t)kWave * NB;
     // as many waves per workgroup as fit (up to NPD_SCF_WPB): fewer workgroups -> fewer counter atomics
     int wpb = NPD_SCF_WPB;
     const size_t red = (size_t)8 * kMaxSeg;  // per wave: n_seg x {bits, blocks} uint32
