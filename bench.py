@@ -238,7 +238,7 @@ def mc_leg(code, snrs, B, cw0, world, timer, dev, ref_counts):
             "config": "Polar(64,32), 2^20 codewords per SNR per GPU, 0-4 dB, one fused launch per sweep"}
 
 
-def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg):
+def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
     """The eval step the metric names (rnn_all.py:853-880): SC and CRISP GRU decode the same words at
     every SNR point and both are counted."""
     from neural_polar_decoder_amd.montecarlo import seeded_crisp
@@ -248,7 +248,7 @@ def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg):
     c_gru = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
 
     def step():
-        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc)
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)  # decoded_SC_msg_bits, rnn_all.py:853
         for si in range(len(snrs)):
             count_errors(msg, dec.decode(net, False, yall[si]), c_gru[si], cols=code.info_positions)
 
@@ -580,7 +580,7 @@ def main():
             ref = allreduce(per_step_counts.to(dev), _sum(), world).cpu()
         legs["montecarlo"] = mc_leg(code, snrs, B, cw0, world, timer, dev, ref)
     if not args.no_gru:
-        legs["sc_plus_gru"] = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg)
+        legs["sc_plus_gru"] = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat)
         legs["crisp_gru"] = gru_leg(code, dev, ys[2], B, world, timer)
         legs["crisp_gru_f512"] = crisp_f512_leg(dev, rank, world, timer)
     if not (args.no_gru and args.no_pac):
