@@ -128,6 +128,18 @@ int npd_sc_decode_lse(const npd_code* code, const float* y, float llr_scale, int
 int npd_sc_decode_soft(const npd_code* code, const float* y, float llr_scale, int hard_decision, const float* priors,
                        float* msg_hat, float* u_bits, int64_t B, void* stream);
 
+/*
+ * PolarCode.sc_decode_soft_new(corrupted_codewords, snr, priors) (polar.py:485-607: updateLLR_soft,
+ * partial_decode_soft, updatePartialSums_soft): SC whose partial sums are LLRs ("soft partial sums",
+ * [a, b] -> [LSE(a, b), b] per stage) -- the decode_soft recursion above -- with the leaf stored as
+ * clamp(L + prior, +-1000) + prior.  Outputs msg_hat (B,K) = sign(stored leaf)[:, info] (the reference's
+ * return value) and optionally u_hat (B,N) = sign of every stored leaf.  priors (N floats, host) or NULL
+ * (zeros: frozen positions are decided like information positions, as in the reference).  Polar codes,
+ * 4 <= N <= 256, y 16-byte aligned.
+ */
+int npd_sc_decode_soft_new(const npd_code* code, const float* y, float llr_scale, const float* priors, float* msg_hat,
+                           float* u_hat, int64_t B, void* stream);
+
 /* ---------------------------------------------------------------------------------- SC-List decode */
 /*
  * Successive-cancellation list decoding, PolarCode.scl_decode(y, snr, L, use_CRC=False)

@@ -42,6 +42,7 @@ SIGNATURES = [
     ("npd_sc_decode_lse", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p, c_i64, c_void_p]),
     ("npd_sc_decode_soft", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p, c_void_p, c_i64,
                                    c_void_p]),
+    ("npd_sc_decode_soft_new", c_int, [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     ("npd_scl_decode", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p, c_i64, c_void_p]),
     ("npd_scl_decode_mc", c_int, [c_void_p, c_void_p, c_float, c_int, c_void_p, c_u64, c_u64, c_i64, c_void_p,
                                   c_void_p]),

@@ -274,7 +274,13 @@ static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
 // PolarCode.sc_decode_soft / decode_soft (polar.py:281-358): the same tree, but every node returns LLRs
 // instead of partial sums -- leaf: L^ = clamp(L + prior, -1000, 1000) (utils.py:259-263 with the 1e-10
 // margins vanishing in fp32), decided sign/tanh; right child input LSE(L^_left, L_a) + L_b; node return
-// [LSE(L^_u, L^_v), L^_v].  No frozen handling (priors carry it).  N <= 64: register-resident;
+// [LSE(L^_u, L^_v), L^_v].  No frozen handling (priors carry it).
+// PolarCode.sc_decode_soft_new (polar.py:485-607) is the same decoder spelled differently: per leaf it
+// re-walks the root-to-leaf path (updateLLR_soft / partial_decode_soft) and rebuilds the "soft partial
+// sums" from the leaf LLRs decided so far (updatePartialSums_soft: stage s replaces [a, b] by
+// [LSE(a, b), b] at stride 2^s), which for every completed block equals the returned-LLR vector above
+// (same operands, same order).  Differences: its leaf stores clamp(L + prior) + prior, and its output is
+// u_hat = sign(stored leaf)[:, info] -- SoftArgs::twice with hard decisions.  N <= 64: register-resident;
 // N = 128, 256: LDS-resident iterative walk (lse_soft_lds_kernel, the layout of lse_sc_kernel).
 struct SoftArgs {
     const float* y;
@@ -283,6 +289,7 @@ struct SoftArgs {
     int64_t B;
     int64_t ntiles;
     float scale;
+    int twice;  // sc_decode_soft_new: the stored leaf LLR is clamp(L + prior) + prior (polar.py:520-546)
     float prior[kMaxN];
 };
 
@@ -291,7 +298,8 @@ __device__ __forceinline__ float clamp1000(float x) { return x < -1000.0f ? -100
 template <int N, bool SOFT, int D, int S0>
 __device__ __forceinline__ void soft_node(RegState<N>& st, const CodeParams& p, const SoftArgs& a, float* ub, float* mh) {
     if constexpr (D == 0) {
-        const float L = clamp1000(st.lv[1] + a.prior[S0]);
+        float L = clamp1000(st.lv[1] + a.prior[S0]);
+        if (a.twice) L = L + a.prior[S0];
         const float u = SOFT ? tanhf(L * 0.5f) : sgnf(L);
         st.beta[S0] = L;
         if (ub) ub[S0] = u;
@@ -390,7 +398,8 @@ __global__ __launch_bounds__(64) void lse_soft_lds_kernel(const CodeParams p, co
                 const int h = 1 << (dd - 1);
                 for (int j = 0; j < h; ++j) LV(h - 1, j) = lse_f(LV(2 * h - 1, j), LV(2 * h - 1, j + h));
             }
-            const float Lf = clamp1000(LV(0, 0) + a.prior[i]);
+            float Lf = clamp1000(LV(0, 0) + a.prior[i]);
+            if (a.twice) Lf = Lf + a.prior[i];
             const float u = SOFT ? tanhf(Lf * 0.5f) : sgnf(Lf);
             BT(i) = Lf;
             if (ub) ub[i] = u;
@@ -466,6 +475,24 @@ extern "C" int npd_sc_decode_lse(const npd_code* code, const float* y, float llr
                          : lse::dispatch<true>(code->p, a, (hipStream_t)stream);
 }
 
+static int soft_entry(const npd_code* code, const float* y, float llr_scale, int hard_decision, int twice,
+                      const float* priors, float* msg_hat, float* u_bits, int64_t B, void* stream) {
+    lse::SoftArgs a{};
+    a.y = y;
+    a.msg = msg_hat;
+    a.ubits = u_bits;
+    a.B = B;
+    a.scale = llr_scale;
+    a.twice = twice;
+    for (int i = 0; i < kMaxN; ++i) a.prior[i] = (priors && i < code->p.N) ? priors[i] : 0.0f;
+    if (getenv("NPD_SOFT_LDS")) {  // force the LDS-resident variant (testing / A-B)
+        return hard_decision ? lse::launch_soft_lds<false>(code->p, a, (hipStream_t)stream)
+                             : lse::launch_soft_lds<true>(code->p, a, (hipStream_t)stream);
+    }
+    return hard_decision ? lse::dispatch_soft<false>(code->p, a, (hipStream_t)stream)
+                         : lse::dispatch_soft<true>(code->p, a, (hipStream_t)stream);
+}
+
 extern "C" int npd_sc_decode_soft(const npd_code* code, const float* y, float llr_scale, int hard_decision,
                                   const float* priors, float* msg_hat, float* u_bits, int64_t B, void* stream) {
     NPD_ARG(code != nullptr, "npd_sc_decode_soft: code is NULL");
@@ -475,17 +502,17 @@ extern "C" int npd_sc_decode_soft(const npd_code* code, const float* y, float ll
     NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_soft: y is NULL");
     NPD_ARG(((uintptr_t)y & 15u) == 0, "npd_sc_decode_soft: y must be 16-byte aligned");
     if (B == 0) return NPD_OK;
-    lse::SoftArgs a{};
-    a.y = y;
-    a.msg = msg_hat;
-    a.ubits = u_bits;
-    a.B = B;
-    a.scale = llr_scale;
-    for (int i = 0; i < kMaxN; ++i) a.prior[i] = (priors && i < code->p.N) ? priors[i] : 0.0f;
-    if (getenv("NPD_SOFT_LDS")) {  // force the LDS-resident variant (testing / A-B)
-        return hard_decision ? lse::launch_soft_lds<false>(code->p, a, (hipStream_t)stream)
-                             : lse::launch_soft_lds<true>(code->p, a, (hipStream_t)stream);
-    }
-    return hard_decision ? lse::dispatch_soft<false>(code->p, a, (hipStream_t)stream)
-                         : lse::dispatch_soft<true>(code->p, a, (hipStream_t)stream);
+    return soft_entry(code, y, llr_scale, hard_decision, 0, priors, msg_hat, u_bits, B, stream);
+}
+
+extern "C" int npd_sc_decode_soft_new(const npd_code* code, const float* y, float llr_scale, const float* priors,
+                                      float* msg_hat, float* u_hat, int64_t B, void* stream) {
+    NPD_ARG(code != nullptr, "npd_sc_decode_soft_new: code is NULL");
+    NPD_ARG(!code->p.pac, "npd_sc_decode_soft_new: Polar codes only (PolarCode.sc_decode_soft_new)");
+    NPD_ARG(code->p.N >= 4 && code->p.N <= kMaxN, "npd_sc_decode_soft_new: 4 <= N <= 256");
+    NPD_ARG(B >= 0, "npd_sc_decode_soft_new: B < 0");
+    NPD_ARG(B == 0 || y != nullptr, "npd_sc_decode_soft_new: y is NULL");
+    NPD_ARG(((uintptr_t)y & 15u) == 0, "npd_sc_decode_soft_new: y must be 16-byte aligned");
+    if (B == 0) return NPD_OK;
+    return soft_entry(code, y, llr_scale, 1, 1, priors, msg_hat, u_hat, B, stream);
 }

@@ -12,6 +12,7 @@ input's device.
   .sc_decode_new(corrupted_codewords, snr, use_gt=None) -> (leaf_llrs, msg_hat) polar.py:465-484
   .sc_decode(noisy_code, snr) -> msg_hat   (exact-LSE SC, hard or soft)         polar.py:209-279
   .sc_decode_soft(noisy_code, snr, priors=None) -> msg_hat  (soft-output SC)     polar.py:281-358
+  .sc_decode_soft_new(y, snr, priors=None) -> decoded_bits  (soft partial sums)   polar.py:485-607
 
 MI355X extras (no reference equivalent, used by the Monte-Carlo driver and bench):
   .mc_generate(B, snr, seed, snr_index, cw_offset)   fused msg -> encode -> AWGN on device
@@ -231,12 +232,7 @@ class PolarCode:
         y = _aligned(_lib.f32c(_lib.stage(noisy_code, "noisy_code")))
         if y.dim() != 2 or y.shape[1] != self.N:
             raise ValueError(f"noisy_code must be (batch, {self.N}), got {tuple(y.shape)}")
-        pr = None
-        if priors is not None:
-            pr = np.ascontiguousarray(np.asarray(priors.cpu() if torch.is_tensor(priors) else priors,
-                                                 dtype=np.float32).reshape(-1))
-            if pr.size != self.N:
-                raise ValueError(f"priors must hold N = {self.N} values")
+        pr = self._priors(priors)
         B = y.shape[0]
         hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
         bits = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_bits else None
@@ -246,6 +242,35 @@ class PolarCode:
                    "npd_sc_decode_soft")
         hat = _lib.home(hat, noisy_code)
         return (hat, _lib.home(bits, noisy_code)) if return_bits else hat
+
+    def _priors(self, priors):
+        if priors is None:
+            return None
+        pr = np.ascontiguousarray(np.asarray(priors.cpu() if torch.is_tensor(priors) else priors,
+                                             dtype=np.float32).reshape(-1))
+        if pr.size != self.N:
+            raise ValueError(f"priors must hold N = {self.N} values")
+        return pr
+
+    def sc_decode_soft_new(self, corrupted_codewords, snr, priors=None, return_u_hat=False):
+        """PolarCode.sc_decode_soft_new (polar.py:592-607, with updateLLR_soft / partial_decode_soft /
+        updatePartialSums_soft, polar.py:485-590): SC with LLR-valued ("soft") partial sums, leaves stored
+        as clamp(L + prior, +-1000) + prior; returns decoded_bits = sign(stored leaf)[:, info] (B,K).
+        priors=None means zeros, so frozen positions are decided like information positions, as in the
+        reference.  ``return_u_hat=True`` also returns u_hat (B,N).  N <= 256."""
+        y = _aligned(_lib.f32c(_lib.stage(corrupted_codewords, "corrupted_codewords")))
+        if y.dim() != 2 or y.shape[1] != self.N:
+            raise ValueError(f"corrupted_codewords must be (batch, {self.N}), got {tuple(y.shape)}")
+        pr = self._priors(priors)
+        B = y.shape[0]
+        hat = torch.empty(B, self.K, dtype=torch.float32, device=y.device)
+        u = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_u_hat else None
+        _lib.check(_lib.load().npd_sc_decode_soft_new(self.code.h, _lib.ptr(y), llr_scale(snr),
+                                                      None if pr is None else pr.ctypes.data_as(ctypes.c_void_p),
+                                                      _lib.ptr(hat), _lib.ptr(u), B, _lib.stream_of(y.device)),
+                   "npd_sc_decode_soft_new")
+        hat = _lib.home(hat, corrupted_codewords)
+        return (hat, _lib.home(u, corrupted_codewords)) if return_u_hat else hat
 
     # ------------------------------------------------------------------ Monte-Carlo extras
     def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False, out=None):

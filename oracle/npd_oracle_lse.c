@@ -15,6 +15,8 @@
  *   log_sum_avoid_zero_NaN         utils.py:348-397  (close_1/close_2 blend written as in the reference)
  *   PolarCode.sc_decode_soft       polar.py:281-358  decode_soft: nodes return LLRs, leaf clamp(L + prior,
  *                                                    +-1000) (Clamp, utils.py:259-263), no frozen rule
+ *   PolarCode.sc_decode_soft_new   polar.py:485-607  the same recursion (see oracle_sc_decode_soft), leaf
+ *                                                    clamp(L + prior) + prior, output sign(leaf)[:, info]
  *
  * Compiled with -ffp-contract=off.  exp/log/tanh are glibc's; torch's CPU path uses Sleef (<= 1 ulp), so
  * agreement with the reference is within a tolerance, pinned by tests/golden/lse_*.npz.
@@ -278,6 +280,8 @@ typedef struct {
     const float* prior;
     int hard;
     float* bits;
+    int twice; /* sc_decode_soft_new: stored leaf = clamp(L + prior) + prior (polar.py:518-546) */
+    float* leaf;
 } soft_ctx;
 
 /* decode_soft(llrs, depth, bit_position, prior) (polar.py:305-358); ret = returned LLR vector (2*half) */
@@ -288,13 +292,19 @@ static void soft_decode(soft_ctx* c, const float* llrs, int depth, int bitpos, f
         float Lu, Luv, Lv, top;
         log_sum_avoid_zero_nan(&llrs[0], &llrs[1], &Lu, 1);
         Lu = clamp1000(Lu + c->prior[lp] * 1.0f);
+        if (c->twice) Lu = Lu + c->prior[lp] * 1.0f;
         float u = c->hard ? sgn(Lu) : tanhf(Lu / 2.0f);
         log_sum_avoid_zero_nan(&Lu, &llrs[0], &Luv, 1);
         Lv = Luv + llrs[1];
         Lv = clamp1000(Lv + c->prior[rp] * 1.0f);
+        if (c->twice) Lv = Lv + c->prior[rp] * 1.0f;
         float v = c->hard ? sgn(Lv) : tanhf(Lv / 2.0f);
         c->bits[lp] = u;
         c->bits[rp] = v;
+        if (c->leaf) {
+            c->leaf[lp] = Lu;
+            c->leaf[rp] = Lv;
+        }
         log_sum_avoid_zero_nan(&Lu, &Lv, &top, 1);
         ret[0] = top;
         ret[1] = Lv;
@@ -310,9 +320,14 @@ static void soft_decode(soft_ctx* c, const float* llrs, int depth, int bitpos, f
     for (int j = 0; j < half; ++j) ret[half + j] = Lhv[j];
 }
 
-/* PolarCode.sc_decode_soft(y, snr, priors): msg_hat = sign(decoded_bits)[:, info]; priors (N) or NULL */
+/* PolarCode.sc_decode_soft(y, snr, priors): msg_hat = sign(decoded_bits)[:, info]; priors (N) or NULL.
+   twice = 1: PolarCode.sc_decode_soft_new (polar.py:485-607), whose per-leaf re-walk of the root-to-leaf
+   path (partial_decode_soft) and rebuilt soft partial sums (updatePartialSums_soft: [a, b] -> [LSE(a, b), b]
+   at stride 2^s over the leaves decided so far, zeros beyond) give, for every completed block, exactly
+   the returned-LLR vectors of this recursion; its leaf stores clamp(L + prior) + prior and its output is
+   sign(stored leaf)[:, info] (call with hard = 1).  leaf_out (B,N): every stored leaf LLR, or NULL. */
 void oracle_sc_decode_soft(const float* y, int64_t B, int N, int K, const int32_t* info, const float* priors,
-                           float llr_scale, int hard, float* msg_hat, float* bits_out) {
+                           float llr_scale, int hard, int twice, float* msg_hat, float* bits_out, float* leaf_out) {
     int n = 0;
     while ((1 << n) < N) ++n;
     float zeros[LSE_MAX_N] = {0};
@@ -321,7 +336,7 @@ void oracle_sc_decode_soft(const float* y, int64_t B, int N, int K, const int32_
     for (int64_t b = 0; b < B; ++b) {
         float llr[LSE_MAX_N], bits[LSE_MAX_N], ret[LSE_MAX_N];
         for (int i = 0; i < N; ++i) llr[i] = llr_scale * y[b * N + i];
-        soft_ctx c = {n, pr, hard, bits};
+        soft_ctx c = {n, pr, hard, bits, twice, leaf_out ? leaf_out + b * N : NULL};
         soft_decode(&c, llr, 0, 0, ret);
         if (bits_out) memcpy(bits_out + b * N, bits, sizeof(float) * (size_t)N);
         if (msg_hat)
@@ -340,6 +355,7 @@ typedef struct {
     double* ebits;
     float* leaf;
     double* eleaf;
+    int twice;
 } softb_ctx;
 
 static inline double add_bound(float a, float b, float r, double ea, double eb) {
@@ -357,6 +373,10 @@ static void softb_decode(softb_ctx* c, const float* llrs, const double* el, int 
         double eLu = lse_bound(llrs[0], llrs[1], Lu0, el[0], el[1]);
         Lu = clamp1000(Lu0 + c->prior[lp] * 1.0f);
         eLu = eLu + U32 * fabs((double)Lu0 + c->prior[lp]);
+        if (c->twice) {
+            Lu = Lu + c->prior[lp] * 1.0f;
+            eLu = eLu + U32 * fabs((double)Lu);
+        }
         float u = c->hard ? sgn(Lu) : tanhf(Lu / 2.0f);
         log_sum_avoid_zero_nan(&Lu, &llrs[0], &Luv, 1);
         const double eLuv = lse_bound(Lu, llrs[0], Luv, eLu, el[0]);
@@ -364,6 +384,10 @@ static void softb_decode(softb_ctx* c, const float* llrs, const double* el, int 
         double eLv = add_bound(Luv, llrs[1], Lv0, eLuv, el[1]);
         Lv = clamp1000(Lv0 + c->prior[rp] * 1.0f);
         eLv = eLv + U32 * fabs((double)Lv0 + c->prior[rp]);
+        if (c->twice) {
+            Lv = Lv + c->prior[rp] * 1.0f;
+            eLv = eLv + U32 * fabs((double)Lv);
+        }
         float v = c->hard ? sgn(Lv) : tanhf(Lv / 2.0f);
         c->bits[lp] = u;
         c->bits[rp] = v;
@@ -399,7 +423,7 @@ static void softb_decode(softb_ctx* c, const float* llrs, const double* el, int 
 }
 
 void oracle_sc_decode_soft_bound(const float* y, int64_t B, int N, const float* priors, float llr_scale, int hard,
-                                 float* bits_out, double* ebits_out, float* leaf_out, double* eleaf_out) {
+                                 int twice, float* bits_out, double* ebits_out, float* leaf_out, double* eleaf_out) {
     int n = 0;
     while ((1 << n) < N) ++n;
     float zeros[LSE_MAX_N] = {0};
@@ -413,7 +437,7 @@ void oracle_sc_decode_soft_bound(const float* y, int64_t B, int N, const float* 
             el[i] = 0.0;
         }
         softb_ctx c = {n, pr, hard, bits_out + b * N, ebits_out + b * N, leaf_out ? leaf_out + b * N : NULL,
-                       eleaf_out ? eleaf_out + b * N : NULL};
+                       eleaf_out ? eleaf_out + b * N : NULL, twice};
         softb_decode(&c, llr, el, 0, 0, ret, eret);
     }
 }

@@ -10,6 +10,7 @@ Every fixture is data: inputs and the reference's outputs for them.  Reference f
   PolarCode.scl_decode (use_CRC=False)                                polar.py:777-876
   PolarCode.sc_decode / decode (exact-LSE SC, hard and soft)          polar.py:209-279
   PolarCode.sc_decode_soft / decode_soft (priors None and random)     polar.py:281-358
+  PolarCode.sc_decode_soft_new (+ stored leaves, priors None / random) polar.py:485-607
   PAC.__init__ / pac_encode / pac_sc_decode                           pac_code.py:97-224, 534-573
   rnn_all.get_code                                                    rnn_all.py:1015-1196
   RNN_Model / RNN_decoder.decode (test branch, y_input, onehot)       rnn_all.py:294-561
@@ -265,6 +266,46 @@ def gen_lse_soft_long():
     gen_lse_soft([(128, 64, 16), (256, 128, 8)], seed=18)
 
 
+def gen_soft_new(cases=None, seed=19):
+    """PolarCode.sc_decode_soft_new (polar.py:485-607), priors None and a frozen-heavy random prior vector:
+    its return value (decoded_bits) and the stored leaf LLRs, obtained by driving the reference's own
+    updateLLR_soft / updatePartialSums_soft per leaf exactly as sc_decode_soft_new does."""
+    rng = np.random.default_rng(seed)
+    for N, K, per in cases or [(16, 8, 32), (32, 16, 32), (64, 32, 24), (128, 64, 8), (256, 128, 4)]:
+        code = polar_code(N, K)
+        code.args = ns(hard_decision=True)  # only feeds partial_decode_soft's unused decoded_bits
+        torch.manual_seed(6000 + N)
+        blocks = []
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (per, K)).float()
+            blocks.append((code.channel(code.encode_plotkin(msg), float(snr)), float(snr)))
+        for snr in (2.0, 4.0):
+            blocks.append((torch.from_numpy(crafted_rows(N, rng)), snr))
+        prior = np.zeros(N, np.float32)
+        prior[np.asarray(code.frozen_positions)] = 20.0
+        prior += rng.standard_normal(N).astype(np.float32)
+        out = {"y": np.concatenate([b.numpy() for b, _ in blocks]),
+               "snr": np.concatenate([np.full(b.shape[0], s) for b, s in blocks]),
+               "info": np.asarray(code.info_positions, np.int64), "prior": prior}
+        info = torch.as_tensor(np.asarray(code.info_positions, np.int64))
+        llrs = torch.cat([(2 / utils_m.snr_db2sigma(snr) ** 2) * y for y, snr in blocks])
+        for ptag, pr in (("p0", None), ("pr", torch.from_numpy(prior))):
+            # sc_decode_soft_new's loop, run once over every block (past the LLR scaling the decoder does
+            # not depend on the SNR), keeping llr_array[:, 0, :] -- the stored leaves
+            prv = torch.zeros(N) if pr is None else pr
+            llr_array, partial = code.define_partial_arrays(llrs)
+            for ii in range(N):
+                llr_array, _ = code.updateLLR_soft(ii, llr_array.clone(), partial, prv)
+                partial = code.updatePartialSums_soft(ii, llr_array[:, 0, :], partial)
+            leaf = llr_array[:, 0, :]
+            out[f"leaf_{ptag}"] = leaf.numpy()
+            out[f"msg_hat_{ptag}"] = torch.sign(leaf)[:, info].numpy()
+            if N <= 32:  # the method itself, block by block, returns the same
+                hats = np.concatenate([code.sc_decode_soft_new(y, snr, priors=pr).numpy() for y, snr in blocks])
+                assert np.array_equal(hats, out[f"msg_hat_{ptag}"])
+        save(f"soft_new_{N}_{K}.npz", **out)
+
+
 def gen_pac():
     rng = np.random.default_rng(6)
     for N, K, per in [(128, 64, 64), (64, 22, 96), (32, 16, 128)]:
@@ -411,6 +452,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "pac", "errors", "gru", "gru_wide", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "conv"]
     for w in which:
         globals()["gen_" + w]()

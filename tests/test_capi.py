@@ -73,6 +73,7 @@ def test_null_pointer_errors_are_reported_not_fatal():
     assert L.npd_count_errors(None, None, 4, 4, None, None) == -1
     assert L.npd_sc_decode_lse(None, None, 1.0, 1, None, None, 16, None) == -1
     assert L.npd_sc_decode_soft(None, None, 1.0, 1, None, None, None, 16, None) == -1
+    assert L.npd_sc_decode_soft_new(None, None, 1.0, None, None, None, 16, None) == -1
 
 
 def test_product_path_has_no_cpu_fallback():

@@ -230,3 +230,66 @@ def test_sc_decode_soft_vs_oracle_random(oracle):
                 h, b = code.sc_decode_soft(t(y), 2.5, priors=prior, hard_decision=hard, return_bits=True)
                 oh, ob = oracle.sc_decode_soft(y, 2.5, info, hard, prior)
                 check(h.cpu().numpy(), b.cpu().numpy(), oh, ob, hard, (N, K, B, hard), soft_bound(y, 2.5, info, prior, hard))
+
+
+def soft_new_bound(y, snr, info, prior):
+    from oracle import oracle as O
+    _, E, leaf, eleaf = O.sc_decode_soft_bound(y, snr, True, prior, leaves=True, twice=True)
+    return {"E": E, "leaf": leaf, "eleaf": eleaf, "info": np.sort(np.asarray(info)), "feedback": False}
+
+
+@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32), (128, 64), (256, 128)])
+def test_sc_decode_soft_new_golden(N, K):
+    """PolarCode.sc_decode_soft_new (polar.py:485-607) vs the reference's vectors: decoded_bits (its return
+    value) and u_hat = sign of every stored leaf.  Its decisions feed nothing (the partial sums are the leaf
+    LLRs), so every disagreement must sit where the stored leaf LLR is within 2 E of zero."""
+    d = golden(f"soft_new_{N}_{K}.npz")
+    code = polar_for(N, d["info"])
+    for ptag in ("p0", "pr"):
+        pr = None if ptag == "p0" else d["prior"]
+        hat = np.empty_like(d[f"msg_hat_{ptag}"])
+        u = np.empty_like(d[f"leaf_{ptag}"])
+        parts = []
+        for s in np.unique(d["snr"]):
+            m = d["snr"] == s
+            h, uh = code.sc_decode_soft_new(t(d["y"][m]), float(s), priors=pr, return_u_hat=True)
+            hat[m], u[m] = h.cpu().numpy(), uh.cpu().numpy()
+            parts.append((m, soft_new_bound(d["y"][m], float(s), d["info"], pr)))
+        check(hat, u, d[f"msg_hat_{ptag}"], np.sign(d[f"leaf_{ptag}"]), True, (N, ptag), stack(parts, d))
+
+
+def test_sc_decode_soft_new_vs_oracle_random(oracle):
+    """Ragged batches, N = 8..256, priors None and frozen-heavy; also host-tensor input (staged to the GPU,
+    result back on the host) and the (B,K) return shape."""
+    from neural_polar_decoder_amd.codes import polar_info_positions
+    for N, K in [(8, 4), (32, 16), (64, 32), (128, 64), (256, 128)]:
+        info = polar_info_positions(N, K)
+        code = polar_for(N, info)
+        rng = np.random.default_rng(5 * N + K)
+        prior = np.zeros(N, np.float32)
+        prior[np.setdiff1d(np.arange(N), info)] = 20.0
+        prior += rng.standard_normal(N).astype(np.float32)
+        for B in (1, 65, 700):
+            y = (rng.standard_normal((B, N)) * 0.8 + (1 - 2 * (rng.random((B, N)) < 0.5))).astype(np.float32)
+            for pr in (None, prior):
+                h, u = code.sc_decode_soft_new(t(y), 2.5, priors=pr, return_u_hat=True)
+                oh, leaf = oracle.sc_decode_soft_new(y, 2.5, info, pr)
+                check(h.cpu().numpy(), u.cpu().numpy(), oh, np.sign(leaf), True, (N, K, B, pr is None),
+                      soft_new_bound(y, 2.5, info, pr))
+        hc = code.sc_decode_soft_new(torch.from_numpy(y), 2.5, priors=torch.from_numpy(prior))
+        assert hc.device.type == "cpu" and hc.shape == (y.shape[0], K)
+        assert torch.equal(hc, code.sc_decode_soft_new(t(y), 2.5, priors=prior).cpu())
+
+
+def test_sc_decode_soft_new_register_and_lds_agree(monkeypatch):
+    """N <= 64 runs the register-resident kernel, NPD_SOFT_LDS=1 the LDS one: identical bits."""
+    from neural_polar_decoder_amd import reference_polar_code
+    for N, K in [(16, 8), (64, 32)]:
+        code = reference_polar_code(N, K)
+        _, _, y = code.mc_generate(2001, 1.0, seed=4, want_msg=False)
+        pr = np.linspace(-3, 3, N).astype(np.float32)
+        h1, u1 = code.sc_decode_soft_new(y, 1.0, priors=pr, return_u_hat=True)
+        monkeypatch.setenv("NPD_SOFT_LDS", "1")
+        h2, u2 = code.sc_decode_soft_new(y, 1.0, priors=pr, return_u_hat=True)
+        monkeypatch.delenv("NPD_SOFT_LDS")
+        assert torch.equal(h1, h2) and torch.equal(u1, u2)

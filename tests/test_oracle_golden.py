@@ -224,3 +224,27 @@ def test_sc_decode_soft_golden(oracle, N, K):
                     m = d["snr"] == s
                     _, _, lf, el = oracle.sc_decode_soft_bound(d["y"][m], float(s), hard, None, leaves=True)
                     assert not oracle.unexplained_disagreements(hat[m], g[m], d["info"], lf, el, False), tag
+
+
+@pytest.mark.parametrize("N,K", [(16, 8), (32, 16), (64, 32), (128, 64), (256, 128)])
+def test_sc_decode_soft_new_golden(oracle, N, K):
+    """PolarCode.sc_decode_soft_new (polar.py:485-607): the oracle restates it as the decode_soft recursion
+    with leaves clamp(L + prior) + prior (npd_oracle_lse.c oracle_sc_decode_soft, twice = 1).  Stored leaf
+    LLRs: every finite one within 2 E of the reference's (oracle.sc_decode_soft_bound, twice=True), same
+    NaN pattern; decoded_bits differ only where the leaf is within 2 E of zero."""
+    d = golden(f"soft_new_{N}_{K}.npz")
+    for ptag in ("p0", "pr"):
+        pr = None if ptag == "p0" else d["prior"]
+        for s in np.unique(d["snr"]):
+            m = d["snr"] == s
+            hat, leaf = oracle.sc_decode_soft_new(d["y"][m], float(s), d["info"], pr)
+            _, _, lf, el = oracle.sc_decode_soft_bound(d["y"][m], float(s), True, pr, leaves=True, twice=True)
+            assert np.array_equal(leaf, lf, equal_nan=True)
+            g = d[f"leaf_{ptag}"][m]
+            fin = np.isfinite(el)
+            assert np.array_equal(np.isnan(leaf[fin]), np.isnan(g[fin])), (N, ptag)
+            ok = ~np.isnan(g) & fin
+            err = np.abs(leaf[ok].astype(np.float64) - g[ok])
+            assert np.all(err <= 2 * el[ok]), (N, ptag, float((err / np.maximum(2 * el[ok], 1e-300)).max()))
+            bad = oracle.unexplained_disagreements(hat, d[f"msg_hat_{ptag}"][m], d["info"], lf, el, False)
+            assert not bad, (N, ptag, bad[:3])

@@ -67,6 +67,8 @@ int main() {
         run<4, false>(ys, outs, ntiles, sink, cus, per_cu, "4-wave WG, read");
         run<1, true>(ys, outs, ntiles, sink, cus, per_cu, "1-wave WG, read+write");
         run<4, true>(ys, outs, ntiles, sink, cus, per_cu, "4-wave WG, read+write");
+        run<8, false>(ys, outs, ntiles, sink, cus, per_cu, "8-wave WG, read");
+        run<8, true>(ys, outs, ntiles, sink, cus, per_cu, "8-wave WG, read+write");
     }
     return 0;
 }
