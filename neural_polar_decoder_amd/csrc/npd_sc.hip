@@ -99,6 +99,7 @@ struct Ctx {
     float beta[R];        // partial sums of the current R-block
     uint32_t S[NW], Z[NW];  // sign / zero bits of partial sums of completed R-blocks (N > R only)
     uint32_t st;          // PAC conv state (bit t = 1 iff state[t] == -1)
+    uint32_t fz[NW];      // frozen-set words, re-read per tile (see the tile loop)
     // LDS row bases (bytes) of this lane
     char* lds;
     uint32_t stage_row;   // staging chunk base for this lane's row (chunk index r*C)
@@ -147,7 +148,7 @@ __device__ __forceinline__ float genie(const Ctx<N, R, PAC, FULL>& c) {
 
 template <int N, int R, bool PAC, bool FULL, int I>
 __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a, float L) {
-    const bool frozen = (p.frozen[I >> 5] >> (I & 31)) & 1u;
+    const bool frozen = (c.fz[I >> 5] >> (I & 31)) & 1u;
     const bool use_gt = FULL && (c.flags & kGt);
     float u;
     if constexpr (!PAC) {
@@ -167,22 +168,18 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& 
                 u = u0;
                 c.st = (c.st << 1) & p.smask;
             }
-        } else {  // pac_code.py:553-568
+        } else {  // pac_code.py:553-568, branch-free: u == u0 -> v = 1, u == -u0 -> v = -1, u == 0 -> v = 0
             u = use_gt ? genie<N, R, PAC, FULL, I>(c) : sgn_bits(L);
-            if (u == u0) {
-                v = 1.0f;
-                c.st = (c.st << 1) & p.smask;
-            } else if (u == -u0) {
-                v = -1.0f;
-                c.st = ((c.st << 1) | 1u) & p.smask;
-            } else {
-                v = 0.0f;
-            }
+            const bool eq = (u == u0), neg = (u == -u0);
+            v = eq ? 1.0f : (neg ? -1.0f : 0.0f);
+            const uint32_t sh = ((c.st << 1) | (neg ? 1u : 0u)) & p.smask;
+            c.st = (eq || neg) ? sh : c.st;
         }
-        lds_wr8(c.lds, c.v_row + I, v);
+        // v is read at information positions only (msg_hat, counts)
+        if (!frozen) lds_wr8(c.lds, c.v_row + I, v);
     }
-    // polar msg-only decoding needs the decisions of information positions only
-    if (PAC || FULL || !frozen) lds_wr8(c.lds, c.u_row + I, u);
+    // u rows: every position for u_hat (FULL); Polar msg-only decoding needs information positions only
+    if (FULL || (!PAC && !frozen)) lds_wr8(c.lds, c.u_row + I, u);
     c.beta[I % R] = u;
 }
 
@@ -214,9 +211,12 @@ __device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL>& c) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int pos = S0 + j;
-        const float b = c.beta[j];
-        const uint32_t sb = (b < 0.0f) ? 1u : 0u;
-        const uint32_t zb = (b == 0.0f) ? 1u : 0u;
+        // b in {+-1, +-0}: sign = bit 31, zero = NOT exponent bit 23 (1.0f = 0x3f800000).  Integer ops,
+        // no compares: compares make 64-bit lane masks that the scheduler parks in VGPR lanes.  A -0's
+        // sign bit is harmless: g_bits returns b outright when the zero bit is set.
+        const uint32_t bb = fbits(c.beta[j]);
+        const uint32_t sb = bb >> 31;
+        const uint32_t zb = (~bb >> 23) & 1u;
         if ((pos & 31) == 0) {
             c.S[pos >> 5] = sb;
             c.Z[pos >> 5] = zb;
@@ -292,10 +292,15 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
         }
         node_up<N, R, PAC, FULL, D - 1, S0>(c, p, a);
         if constexpr ((1 << D) == N) {
+            // second read of the row (L2 / MALL).  The pointer is laundered through an empty asm so the
+            // compiler cannot forward the f step's loads: keeping those N values live across the left
+            // half would cost N VGPRs (N = 128: 384 instead of ~250 -> one wave per SIMD instead of two)
+            const float4* yr = c.yrow;
+            asm volatile("" : "+v"(yr));
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 A = c.yrow[q];  // second read of the row: L2 / MALL
-                const float4 Bv = c.yrow[q + h / 4];
+                const float4 A = yr[q];
+                const float4 Bv = yr[q + h / 4];
                 const float av[4] = {A.x, A.y, A.z, A.w};
                 const float bv[4] = {Bv.x, Bv.y, Bv.z, Bv.w};
 #pragma unroll
@@ -356,9 +361,9 @@ __device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint3
 }
 
 // ------------------------------------------------------------------------------ kernel
-// N <= 64: every LLR level in VGPRs; ask for <= 256 VGPRs so two waves share each SIMD
+// <= 256 VGPRs so two waves share each SIMD (N = 256 is LDS-bound at 3 waves per CU anyway)
 template <int N, int R, bool PAC, bool FULL>
-__global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kernel(const CodeParams p, const Args a) {
+__global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
     constexpr int C = Geo<N>::C;
@@ -429,6 +434,14 @@ __global__ __launch_bounds__(64, (N <= 64 ? NPD_SC_WPE : 1)) void sc_decode_kern
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
         c.st = 0;
+        // The frozen words are loop-invariant, so LICM would hoist all N per-leaf frozen tests out of the
+        // tile loop as 64-bit lane masks and spill them into VGPR lanes (two v_readlane per leaf, plus
+        // scratch); an opaque per-tile copy keeps each test next to its leaf (one s_bitcmp).
+#pragma unroll
+        for (int w = 0; w < Ctx<N, R, PAC, FULL>::NW; ++w) {
+            c.fz[w] = p.frozen[w];
+            asm volatile("" : "+s"(c.fz[w]));
+        }
         if constexpr (R == N) {
             // whole row into registers
 #pragma unroll
