@@ -182,17 +182,37 @@ template <int N>
 struct RegState {
     float lv[2 * N];
     float beta[N];
+    uint32_t fz[(N + 31) / 32];  // frozen words, re-read opaquely per tile
+    int k;                       // information leaves decided so far (= msg_hat column; info is sorted)
 };
+
+// Per-tile opaque copies of the loop-invariant frozen words: left alone, LICM hoists every per-leaf frozen
+// test (a 64-bit lane mask) out of the tile loop and parks them in VGPR lanes (hundreds of v_writelane /
+// v_readlane per tile at N = 64).  Priors are read per leaf at an opaque index for the same reason (an
+// escaped pointer to the by-value argument would copy it to scratch instead).
+template <int N>
+__device__ __forceinline__ void opaque_code(RegState<N>& st, const CodeParams& p) {
+#pragma unroll
+    for (int w = 0; w < (N + 31) / 32; ++w) {
+        uint32_t fw = p.frozen[w];
+        asm volatile("" : "+s"(fw));
+        st.fz[w] = fw;
+    }
+    st.k = 0;
+}
 
 template <int N, bool SOFT, int D, int S0>
 __device__ __forceinline__ void reg_node(RegState<N>& st, const CodeParams& p, float* ub, float* mh) {
     if constexpr (D == 0) {
-        const bool frozen = (p.frozen[S0 >> 5] >> (S0 & 31)) & 1u;
+        const bool frozen = (st.fz[S0 >> 5] >> (S0 & 31)) & 1u;
         float u = 1.0f;
         if (!frozen) u = SOFT ? tanhf(st.lv[1] * 0.5f) : sgnf(st.lv[1]);
         st.beta[S0] = u;
         if (ub) ub[S0] = u;
-        if (mh && !frozen) mh[p.rank[S0]] = sgnf(u);
+        if (!frozen) {
+            if (mh) mh[st.k] = sgnf(u);
+            ++st.k;
+        }
     } else {
         constexpr int h = 1 << (D - 1);
 #pragma unroll
@@ -225,6 +245,7 @@ __global__ __launch_bounds__(64) void lse_sc_reg_kernel(const CodeParams p, cons
         float* ub = (a.ubits && valid) ? a.ubits + row * N : nullptr;
         float* mh = (a.msg && valid) ? a.msg + row * p.K : nullptr;
         RegState<N> st;
+        opaque_code(st, p);
         const float4* yr = reinterpret_cast<const float4*>(a.y + r * N);
 #pragma unroll
         for (int q = 0; q < N / 4; ++q) {
@@ -298,13 +319,19 @@ __device__ __forceinline__ float clamp1000(float x) { return x < -1000.0f ? -100
 template <int N, bool SOFT, int D, int S0>
 __device__ __forceinline__ void soft_node(RegState<N>& st, const CodeParams& p, const SoftArgs& a, float* ub, float* mh) {
     if constexpr (D == 0) {
-        float L = clamp1000(st.lv[1] + a.prior[S0]);
-        if (a.twice) L = L + a.prior[S0];
+        int ix = S0;
+        asm volatile("" : "+s"(ix));
+        const float pr = a.prior[ix];
+        float L = clamp1000(st.lv[1] + pr);
+        if (a.twice) L = L + pr;
         const float u = SOFT ? tanhf(L * 0.5f) : sgnf(L);
         st.beta[S0] = L;
         if (ub) ub[S0] = u;
-        const bool frozen = (p.frozen[S0 >> 5] >> (S0 & 31)) & 1u;
-        if (mh && !frozen) mh[p.rank[S0]] = sgnf(u);
+        const bool frozen = (st.fz[S0 >> 5] >> (S0 & 31)) & 1u;
+        if (!frozen) {
+            if (mh) mh[st.k] = sgnf(u);
+            ++st.k;
+        }
     } else {
         constexpr int h = 1 << (D - 1);
 #pragma unroll
@@ -330,6 +357,7 @@ __global__ __launch_bounds__(64) void lse_soft_sc_kernel(const CodeParams p, con
         float* ub = (a.ubits && valid) ? a.ubits + row * N : nullptr;
         float* mh = (a.msg && valid) ? a.msg + row * p.K : nullptr;
         RegState<N> st;
+        opaque_code(st, p);
         const float4* yr = reinterpret_cast<const float4*>(a.y + r * N);
 #pragma unroll
         for (int q = 0; q < N / 4; ++q) {

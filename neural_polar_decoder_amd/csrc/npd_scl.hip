@@ -141,8 +141,11 @@ __device__ __forceinline__ void copy_live(Lane<N, G>& c, int src) {
 }
 
 // survivors of pruneLists for one group when a metric tie straddles the L-th place (rare): exact rule
+// km / fm arrive as 8-wide vectors (VGPRs): arrays passed by reference would live in scratch, stored at
+// every information leaf whether or not the tie path is taken
+typedef float f8v __attribute__((ext_vector_type(8)));
 template <int G>
-__device__ __noinline__ uint32_t exact_mask(const float (&km)[G], const float (&fm)[G], int s, int L) {
+__device__ __noinline__ uint32_t exact_mask(f8v km, f8v fm, int s, int L) {
     float negm[16];
 #pragma unroll
     for (int t = 0; t < G; ++t) {
@@ -203,7 +206,15 @@ __device__ __forceinline__ uint32_t list_select(float m, float a, int j, int bl,
     uint32_t msel = ((uint32_t)(bk >> bl) & lowm) | (((uint32_t)(bf >> bl) & lowm) << s);
     if (bs) {
         const bool mine = ((uint32_t)(bs >> bl) & ((G >= 32) ? 0xFFFFFFFFu : ((1u << G) - 1u))) != 0u;
-        if (mine) msel = exact_mask<G>(km, fm, s, L);
+        if (mine) {
+            f8v kv = {}, fv = {};
+#pragma unroll
+            for (int t = 0; t < G; ++t) {
+                kv[t] = km[t];
+                fv[t] = fm[t];
+            }
+            msel = exact_mask<G>(kv, fv, s, L);
+        }
     }
     return msel;
 }
