@@ -149,7 +149,10 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
 #define NPD_GRU_BF_WPB 4
 #endif
 
-template <int F, int L, int WPB>
+// OVL (2 layers): layer 1's recurrent product W_hh1 h1 reads the OLD h1 only, so it is issued right after
+// layer 0's GEMM and its MFMAs run while layer 0's gate update (VALU + transcendentals) executes; the
+// input product W_ih1 h0' follows the update, accumulated onto the r/z rows of W_hh1 h1.
+template <int F, int L, int WPB, bool OVL = false>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
@@ -205,6 +208,45 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             const float xbe = half ? xb : 1.0f;  // extra k-step B operand: [1, x_i]
+            if constexpr (L == 2 && OVL) {
+                f16v acc[TT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
+#pragma unroll
+                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
+                // gh = W_hh1 h1 (old state): independent of layer 0's update below
+                f16v gh[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) gh[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 2, 0, lane, gh, h1);
+#pragma unroll
+                for (int j = 0; j < HT; ++j)
+                    gh[2 * HT + j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, gh[2 * HT + j]);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
+                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                }
+                // r, z: W_ih1 h0' accumulated onto gh (gi + gh); n: gin = W_ih1_n h0' kept apart (r * (W_hh1_n h1))
+                f16v arz[2 * HT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) arz[t] = gh[t];
+                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 1, 0, lane, arz, h0);
+                f16v gin[HT];
+#pragma unroll
+                for (int j = 0; j < HT; ++j) gin[j] = zero;
+                gemm_chain<TT, KG, HT, HT>(smem4, 1, 2 * HT, lane, gin, h0);
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) arz[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, arz[t]);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    gin[j] = mfma(smem[G::OFF_X + (TT + 2 * HT + j) * 64 + lane], one_or_zero, gin[j]);
+                    gru_update(h1[j], arz[j], arz[HT + j], gin[j], gh[2 * HT + j]);
+                }
+            } else {
             // ================= layer 0: acc = P + W_hh0 h0 + consts + x_i column
             {
                 f16v acc[TT];
@@ -243,6 +285,7 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                     gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             }
+            }  // !OVL
             // ================= output: Linear(F, 1) on the top layer
             float part = 0.0f;
 #pragma unroll
@@ -350,10 +393,10 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L, int WPB>
+template <int F, int L, int WPB, bool OVL = false>
 static int launch_w(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
-    auto kern = gru_decode_kernel<F, L, WPB>;
+    auto kern = gru_decode_kernel<F, L, WPB, OVL>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -376,10 +419,24 @@ static int gru_waves() {
     return w;
 }
 
+// layer-1 overlap schedule (OVL); NPD_GRU_OVL=0/1 A/B
+static bool gru_ovl() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NPD_GRU_OVL");
+        v = (e && *e) ? (e[0] == '1') : 0;
+    }
+    return v == 1;
+}
+
 template <int F, int L>
 static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
     (void)g;
-    return gru_waves() == 4 ? launch_w<F, L, 4>(a, s) : launch_w<F, L, 8>(a, s);
+    if (gru_waves() == 8) return launch_w<F, L, 8>(a, s);
+    if constexpr (L == 2) {
+        if (gru_ovl()) return launch_w<F, L, 4, true>(a, s);
+    }
+    return launch_w<F, L, 4>(a, s);
 }
 
 

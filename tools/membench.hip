@@ -8,13 +8,15 @@
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-template <int WPG, bool STORE, int UNROLL>
+template <int WPG, bool STORE, int UNROLL, bool ILV = false>
 __global__ __launch_bounds__(64 * WPG) void stream_kernel(const f4* __restrict__ y, f4* __restrict__ out, long ntiles,
                                                            float* sink) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     f4 acc = {0, 0, 0, 0};
-    for (long t = (long)blockIdx.x * WPG + wave; t < ntiles; t += (long)gridDim.x * WPG) {
+    // ILV: adjacent tiles go to consecutive workgroups (round-robin over XCDs) instead of one workgroup's waves
+    const long t0 = ILV ? (long)wave * gridDim.x + blockIdx.x : (long)blockIdx.x * WPG + wave;
+    for (long t = t0; t < ntiles; t += (long)gridDim.x * WPG) {
         f4 v[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) v[q] = y[t * 1024 + lane + 64 * q];
@@ -28,18 +30,18 @@ __global__ __launch_bounds__(64 * WPG) void stream_kernel(const f4* __restrict__
     if (acc.x == 123.456f) sink[0] = acc.y;
 }
 
-template <int WPG, bool STORE>
+template <int WPG, bool STORE, bool ILV = false>
 static void run(f4** ys, f4** outs, long ntiles, float* sink, int cus, int per_cu, const char* name) {
     int grid = cus * per_cu / WPG;
     if (grid < 1) grid = 1;
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int w = 0; w < 2; ++w) hipLaunchKernelGGL((stream_kernel<WPG, STORE, 1>), dim3(grid), dim3(64 * WPG), 0, 0, ys[w % 5], outs[w % 5], ntiles, sink);
+    for (int w = 0; w < 2; ++w) hipLaunchKernelGGL((stream_kernel<WPG, STORE, 1, ILV>), dim3(grid), dim3(64 * WPG), 0, 0, ys[w % 5], outs[w % 5], ntiles, sink);
     hipEventRecord(a);
     const int it = 10;
     for (int i = 0; i < it; ++i)
-        hipLaunchKernelGGL((stream_kernel<WPG, STORE, 1>), dim3(grid), dim3(64 * WPG), 0, 0, ys[i % 5], outs[i % 5], ntiles, sink);
+        hipLaunchKernelGGL((stream_kernel<WPG, STORE, 1, ILV>), dim3(grid), dim3(64 * WPG), 0, 0, ys[i % 5], outs[i % 5], ntiles, sink);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -69,6 +71,8 @@ int main() {
         run<4, true>(ys, outs, ntiles, sink, cus, per_cu, "4-wave WG, read+write");
         run<8, false>(ys, outs, ntiles, sink, cus, per_cu, "8-wave WG, read");
         run<8, true>(ys, outs, ntiles, sink, cus, per_cu, "8-wave WG, read+write");
+        run<8, false, true>(ys, outs, ntiles, sink, cus, per_cu, "8-wave WG ilv, read");
+        run<8, true, true>(ys, outs, ntiles, sink, cus, per_cu, "8-wave WG ilv, read+write");
     }
     return 0;
 }
