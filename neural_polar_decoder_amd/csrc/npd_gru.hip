@@ -152,7 +152,7 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
 // OVL (2 layers): layer 1's recurrent product W_hh1 h1 reads the OLD h1 only, so it is issued right after
 // layer 0's GEMM and its MFMAs run while layer 0's gate update (VALU + transcendentals) executes; the
 // input product W_ih1 h0' follows the update, accumulated onto the r/z rows of W_hh1 h1.
-template <int F, int L, int WPB, bool OVL = false>
+template <int F, int L, int WPB, int OVL = 0>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             const float xbe = half ? xb : 1.0f;  // extra k-step B operand: [1, x_i]
-            if constexpr (L == 2 && OVL) {
+            if constexpr (L == 2 && OVL == 1) {
                 f16v acc[TT];
 #pragma unroll
                 for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
@@ -245,6 +245,41 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                 for (int j = 0; j < HT; ++j) {
                     gin[j] = mfma(smem[G::OFF_X + (TT + 2 * HT + j) * 64 + lane], one_or_zero, gin[j]);
                     gru_update(h1[j], arz[j], arz[HT + j], gin[j], gh[2 * HT + j]);
+                }
+            } else if constexpr (L == 2 && OVL == 2) {
+                // only the n rows of W_hh1 h1 (64 MFMAs, about the length of the gate update) are issued
+                // ahead; everything else keeps the plain order, so results are bit-identical to OVL = 0
+                f16v acc[TT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
+#pragma unroll
+                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
+                f16v ahn[HT];
+#pragma unroll
+                for (int j = 0; j < HT; ++j) ahn[j] = zero;
+                gemm_chain<TT, KG, HT, HT>(smem4, 2, 2 * HT, lane, ahn, h1);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
+                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                }
+                f16v acc1[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
+                f16v arz[2 * HT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
+                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 2, 0, lane, arz, h1);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
+                    gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             } else {
             // ================= layer 0: acc = P + W_hh0 h0 + consts + x_i column
@@ -393,7 +428,7 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L, int WPB, bool OVL = false>
+template <int F, int L, int WPB, int OVL = 0>
 static int launch_w(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
     auto kern = gru_decode_kernel<F, L, WPB, OVL>;
@@ -419,14 +454,10 @@ static int gru_waves() {
     return w;
 }
 
-// layer-1 overlap schedule (OVL); NPD_GRU_OVL=0/1 A/B
-static bool gru_ovl() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_GRU_OVL");
-        v = (e && *e) ? (e[0] == '1') : 0;
-    }
-    return v == 1;
+// layer-1 overlap schedule (OVL: 0 plain, 1 all of W_hh1 h1 ahead, 2 its n rows ahead); NPD_GRU_OVL A/B
+static int gru_ovl() {  // read per launch (tests switch it)
+    const char* e = getenv("NPD_GRU_OVL");
+    return (e && *e >= '0' && *e <= '2') ? (*e - '0') : 0;
 }
 
 template <int F, int L>
@@ -434,7 +465,8 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
     (void)g;
     if (gru_waves() == 8) return launch_w<F, L, 8>(a, s);
     if constexpr (L == 2) {
-        if (gru_ovl()) return launch_w<F, L, 4, true>(a, s);
+        if (gru_ovl() == 1) return launch_w<F, L, 4, 1>(a, s);
+        if (gru_ovl() == 2) return launch_w<F, L, 4, 2>(a, s);
     }
     return launch_w<F, L, 4>(a, s);
 }
