@@ -204,6 +204,16 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
         }
         float xb = 1.0f;  // x_i: onehot index of the previous decision (or its sign); step 0: prev = +1
         const float one_or_zero = half ? 0.0f : 1.0f;
+        // OVL == 3: layer 0's recurrent GEMM of step i+1 (needs only h0 of step i) is issued during step
+        // i's layer-1 gate update; acc0 carries it across the iteration boundary
+        f16v acc0[TT];
+        if constexpr (L == 2 && OVL == 3) {
+#pragma unroll
+            for (int t = 0; t < 2 * HT; ++t) acc0[t] = P[t];
+#pragma unroll
+            for (int t = 2 * HT; t < TT; ++t) acc0[t] = zero;
+            gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc0, h0);
+        }
 
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
@@ -245,6 +255,40 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                 for (int j = 0; j < HT; ++j) {
                     gin[j] = mfma(smem[G::OFF_X + (TT + 2 * HT + j) * 64 + lane], one_or_zero, gin[j]);
                     gru_update(h1[j], arz[j], arz[HT + j], gin[j], gh[2 * HT + j]);
+                }
+            } else if constexpr (L == 2 && OVL == 3) {
+                f16v acc[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc0[t]);
+                f16v ahn[HT];
+#pragma unroll
+                for (int j = 0; j < HT; ++j) ahn[j] = zero;
+                gemm_chain<TT, KG, HT, HT>(smem4, 2, 2 * HT, lane, ahn, h1);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
+                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                }
+                f16v acc1[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
+                f16v arz[2 * HT];
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
+                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 2, 0, lane, arz, h1);
+                // next step's layer-0 GEMM (h0 is final for this step) alongside layer 1's update
+#pragma unroll
+                for (int t = 0; t < 2 * HT; ++t) acc0[t] = P[t];
+#pragma unroll
+                for (int t = 2 * HT; t < TT; ++t) acc0[t] = zero;
+                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc0, h0);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) {
+                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
+                    gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             } else if constexpr (L == 2 && OVL == 2) {
                 // only the n rows of W_hh1 h1 (64 MFMAs, about the length of the gate update) are issued
@@ -454,10 +498,11 @@ static int gru_waves() {
     return w;
 }
 
-// layer-1 overlap schedule (OVL: 0 plain, 1 all of W_hh1 h1 ahead, 2 its n rows ahead); NPD_GRU_OVL A/B
+// overlap schedule (OVL: 0 plain, 1 all of W_hh1 h1 ahead, 2 its n rows ahead, 3 = 2 + the next step's
+// layer-0 GEMM during layer 1's update); NPD_GRU_OVL A/B
 static int gru_ovl() {  // read per launch (tests switch it)
     const char* e = getenv("NPD_GRU_OVL");
-    return (e && *e >= '0' && *e <= '2') ? (*e - '0') : 0;
+    return (e && *e >= '0' && *e <= '3') ? (*e - '0') : 0;
 }
 
 template <int F, int L>
@@ -467,6 +512,7 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
     if constexpr (L == 2) {
         if (gru_ovl() == 1) return launch_w<F, L, 4, 1>(a, s);
         if (gru_ovl() == 2) return launch_w<F, L, 4, 2>(a, s);
+        if (gru_ovl() == 3) return launch_w<F, L, 4, 3>(a, s);
     }
     return launch_w<F, L, 4>(a, s);
 }
