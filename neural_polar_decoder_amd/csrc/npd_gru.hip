@@ -149,10 +149,7 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
 #define NPD_GRU_BF_WPB 4
 #endif
 
-// OVL (2 layers): layer 1's recurrent product W_hh1 h1 reads the OLD h1 only, so it is issued right after
-// layer 0's GEMM and its MFMAs run while layer 0's gate update (VALU + transcendentals) executes; the
-// input product W_ih1 h0' follows the update, accumulated onto the r/z rows of W_hh1 h1.
-template <int F, int L, int WPB, int OVL = 0>
+template <int F, int L, int WPB>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
@@ -204,128 +201,10 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
         }
         float xb = 1.0f;  // x_i: onehot index of the previous decision (or its sign); step 0: prev = +1
         const float one_or_zero = half ? 0.0f : 1.0f;
-        // OVL == 3: layer 0's recurrent GEMM of step i+1 (needs only h0 of step i) is issued during step
-        // i's layer-1 gate update; acc0 carries it across the iteration boundary
-        f16v acc0[TT];
-        if constexpr (L == 2 && OVL == 3) {
-#pragma unroll
-            for (int t = 0; t < 2 * HT; ++t) acc0[t] = P[t];
-#pragma unroll
-            for (int t = 2 * HT; t < TT; ++t) acc0[t] = zero;
-            gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc0, h0);
-        }
 
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             const float xbe = half ? xb : 1.0f;  // extra k-step B operand: [1, x_i]
-            if constexpr (L == 2 && OVL == 1) {
-                f16v acc[TT];
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
-#pragma unroll
-                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
-                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
-                // gh = W_hh1 h1 (old state): independent of layer 0's update below
-                f16v gh[TT];
-#pragma unroll
-                for (int t = 0; t < TT; ++t) gh[t] = zero;
-                gemm_chain<TT, KG, TT, HT>(smem4, 2, 0, lane, gh, h1);
-#pragma unroll
-                for (int j = 0; j < HT; ++j)
-                    gh[2 * HT + j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, gh[2 * HT + j]);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) {
-                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
-                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
-                }
-                // r, z: W_ih1 h0' accumulated onto gh (gi + gh); n: gin = W_ih1_n h0' kept apart (r * (W_hh1_n h1))
-                f16v arz[2 * HT];
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) arz[t] = gh[t];
-                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 1, 0, lane, arz, h0);
-                f16v gin[HT];
-#pragma unroll
-                for (int j = 0; j < HT; ++j) gin[j] = zero;
-                gemm_chain<TT, KG, HT, HT>(smem4, 1, 2 * HT, lane, gin, h0);
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) arz[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, arz[t]);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) {
-                    gin[j] = mfma(smem[G::OFF_X + (TT + 2 * HT + j) * 64 + lane], one_or_zero, gin[j]);
-                    gru_update(h1[j], arz[j], arz[HT + j], gin[j], gh[2 * HT + j]);
-                }
-            } else if constexpr (L == 2 && OVL == 3) {
-                f16v acc[TT];
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc0[t]);
-                f16v ahn[HT];
-#pragma unroll
-                for (int j = 0; j < HT; ++j) ahn[j] = zero;
-                gemm_chain<TT, KG, HT, HT>(smem4, 2, 2 * HT, lane, ahn, h1);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) {
-                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
-                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
-                }
-                f16v acc1[TT];
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc1[t] = zero;
-                gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
-                f16v arz[2 * HT];
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
-                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 2, 0, lane, arz, h1);
-                // next step's layer-0 GEMM (h0 is final for this step) alongside layer 1's update
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) acc0[t] = P[t];
-#pragma unroll
-                for (int t = 2 * HT; t < TT; ++t) acc0[t] = zero;
-                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc0, h0);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) {
-                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
-                    gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
-                }
-            } else if constexpr (L == 2 && OVL == 2) {
-                // only the n rows of W_hh1 h1 (64 MFMAs, about the length of the gate update) are issued
-                // ahead; everything else keeps the plain order, so results are bit-identical to OVL = 0
-                f16v acc[TT];
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
-#pragma unroll
-                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
-                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
-                f16v ahn[HT];
-#pragma unroll
-                for (int j = 0; j < HT; ++j) ahn[j] = zero;
-                gemm_chain<TT, KG, HT, HT>(smem4, 2, 2 * HT, lane, ahn, h1);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) {
-                    const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
-                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
-                }
-                f16v acc1[TT];
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc1[t] = zero;
-                gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
-#pragma unroll
-                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
-                f16v arz[2 * HT];
-#pragma unroll
-                for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
-                gemm_chain<TT, KG, 2 * HT, HT>(smem4, 2, 0, lane, arz, h1);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) {
-                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
-                    gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
-                }
-            } else {
             // ================= layer 0: acc = P + W_hh0 h0 + consts + x_i column
             {
                 f16v acc[TT];
@@ -364,7 +243,6 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                     gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             }
-            }  // !OVL
             // ================= output: Linear(F, 1) on the top layer
             float part = 0.0f;
 #pragma unroll
@@ -472,10 +350,10 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L, int WPB, int OVL = 0>
+template <int F, int L, int WPB>
 static int launch_w(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
-    auto kern = gru_decode_kernel<F, L, WPB, OVL>;
+    auto kern = gru_decode_kernel<F, L, WPB>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -498,23 +376,10 @@ static int gru_waves() {
     return w;
 }
 
-// overlap schedule (OVL: 0 plain, 1 all of W_hh1 h1 ahead, 2 its n rows ahead, 3 = 2 + the next step's
-// layer-0 GEMM during layer 1's update); NPD_GRU_OVL A/B
-static int gru_ovl() {  // read per launch (tests switch it)
-    const char* e = getenv("NPD_GRU_OVL");
-    return (e && *e >= '0' && *e <= '3') ? (*e - '0') : 0;
-}
-
 template <int F, int L>
 static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
     (void)g;
-    if (gru_waves() == 8) return launch_w<F, L, 8>(a, s);
-    if constexpr (L == 2) {
-        if (gru_ovl() == 1) return launch_w<F, L, 4, 1>(a, s);
-        if (gru_ovl() == 2) return launch_w<F, L, 4, 2>(a, s);
-        if (gru_ovl() == 3) return launch_w<F, L, 4, 3>(a, s);
-    }
-    return launch_w<F, L, 4>(a, s);
+    return gru_waves() == 4 ? launch_w<F, L, 4>(a, s) : launch_w<F, L, 8>(a, s);
 }
 
 

@@ -62,33 +62,6 @@ def test_gru_vs_oracle_large(oracle):
     assert np.abs(logits[same] - ol[same]).max() < LOGIT_ATOL
 
 
-@pytest.mark.parametrize("mode", ["1", "2", "3"])
-def test_gru_overlap_schedules(monkeypatch, mode):
-    """NPD_GRU_OVL=2 (n rows of W_hh1 h1 issued ahead) and 3 (also the next step's layer-0 GEMM during
-    layer 1's update) only reorder independent MFMAs: bit-identical to the plain order; NPD_GRU_OVL=1 also sums the W_ih1 and W_hh1 products in another order: logits within
-    LOGIT_ATOL on agreeing codewords.  Both against the golden fixture too."""
-    d = golden("gru_polar_64_32.npz")
-    net, dec = build(d)
-    from neural_polar_decoder_amd import reference_polar_code
-    code = reference_polar_code(64, 32)
-    _, _, y = code.mc_generate(2000 + 33, 1.0, seed=5, device=DEV, want_msg=False)
-    monkeypatch.setenv("NPD_GRU_OVL", "0")
-    o0, l0 = dec.decode(net, False, y, return_logits=True)
-    monkeypatch.setenv("NPD_GRU_OVL", mode)
-    o1, l1 = dec.decode(net, False, y, return_logits=True)
-    if mode in ("2", "3"):
-        assert torch.equal(o0, o1) and torch.equal(l0, l1)
-    else:
-        same = (o0 == o1).all(1)
-        assert same.float().mean().item() >= 0.99
-        assert (l0[same] - l1[same]).abs().max().item() < LOGIT_ATOL
-    yg = torch.from_numpy(d["y"]).to(DEV)
-    out, logits = dec.decode(net, False, yg, return_logits=True)
-    same = (out.cpu().numpy() == d["decoded"]).all(1)
-    assert same.mean() >= 0.99
-    assert np.abs(logits.cpu().numpy()[same] - d["logits"][same]).max() < LOGIT_ATOL
-
-
 def test_gru_genie_frozen_values():
     """gt given: frozen positions keep gt's values (rnn_all.py:528-530), info positions are decided."""
     d = golden("gru_polar_64_32.npz")
