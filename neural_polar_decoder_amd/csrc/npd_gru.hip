@@ -122,20 +122,40 @@ __device__ __forceinline__ float fast_tanh(float x) { return fmaf(2.0f, fast_sig
 
 // PyTorch GRUCell update on one 32x32 tile pair: h = (h - n) * z + n,
 // r = sigmoid(a_r), z = sigmoid(a_z), n = tanh(a_in + r * a_hn)
+// The fp32 MFMAs and this VALU work do not co-issue (PMC: MFMA-busy + VALU-active ~ 1), so the update's
+// instruction count is on the critical path: element pairs go through v_pk_mul/add/fma_f32 (two lanes'
+// worth of fp32 per instruction); only exp2 / rcp stay scalar.  Same operations and rounding per element.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v exp2_2(f2v x) { return f2v{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
+__device__ __forceinline__ f2v rcp_2(f2v x) { return f2v{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
+
 __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
+#if NPD_GRU_PRECISE_GATES
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-#if NPD_GRU_PRECISE_GATES
         const float r = sigmoidf_(ar[i]);
         const float z = sigmoidf_(az[i]);
         const float nn = tanhf(ain[i] + ahn[i] * r);
-#else
-        const float r = fast_sigmoid(ar[i]);
-        const float z = fast_sigmoid(az[i]);
-        const float nn = fast_tanh(ain[i] + ahn[i] * r);
-#endif
         h[i] = (h[i] - nn) * z + nn;
     }
+#else
+    const f2v one = {1.0f, 1.0f};
+    const f2v ml2e = {-1.44269504088896340736f, -1.44269504088896340736f};
+    const f2v two = {2.0f, 2.0f};
+    const f2v m2l2e = {-2.88539008177792681472f, -2.88539008177792681472f};  // (2x)(-log2 e) == x(-2 log2 e), both exact scalings
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+        const f2v r = rcp_2(one + exp2_2(ml2e * f2v{ar[i], ar[i + 1]}));
+        const f2v z = rcp_2(one + exp2_2(ml2e * f2v{az[i], az[i + 1]}));
+        const f2v x = f2v{ain[i], ain[i + 1]} + f2v{ahn[i], ahn[i + 1]} * r;
+        const f2v s2 = rcp_2(one + exp2_2(m2l2e * x));
+        const f2v nn = __builtin_elementwise_fma(two, s2, -one);
+        const f2v hv = f2v{h[i], h[i + 1]};
+        const f2v hn = (hv - nn) * z + nn;
+        h[i] = hn.x;
+        h[i + 1] = hn.y;
+    }
+#endif
 }
 
 // Waves per workgroup of the F <= 64 kernels: all share the workgroup's LDS copy of the weights.  8 waves
