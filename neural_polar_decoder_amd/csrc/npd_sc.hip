@@ -91,8 +91,31 @@ struct Geo {
     static constexpr int NB = 4 * ((N / 4) | 1);  // byte-row stride: an odd number of dwords (conflict-free)
 };
 
+// ------------------------------------------------------------------------------ frozen set
+// NoSpec: the frozen set is read at run time (CodeParams).  Spec<M0, M1>: known at compile time (the
+// reference's standard PAC(128,64) 'RM' profile) -- every frozen test is static, and in msg-only PAC decoding
+// a rate-0 subtree needs no LLRs at all: its decisions are the convolution's output for v = +1
+// (pac_code.py:545-551), whatever the channel says, so the f/g steps feeding it are skipped.
+struct NoSpec {
+    static constexpr bool on = false;
+    static constexpr bool frozen(int) { return false; }
+    static constexpr bool rate0(int, int) { return false; }
+};
+template <uint64_t M0, uint64_t M1>
+struct Spec {
+    static constexpr bool on = true;
+    static constexpr bool frozen(int i) { return (((i < 64) ? (M0 >> i) : (M1 >> (i - 64))) & 1ull) != 0; }
+    static constexpr bool rate0(int s0, int len) {
+        for (int i = s0; i < s0 + len; ++i)
+            if (!frozen(i)) return false;
+        return true;
+    }
+};
+// PAC(128,64), 'RM' rate profile (popcount(i) < 4 frozen; pac_code.py:121-174)
+using SpecPacRm128 = Spec<0x117177f177f7fffull, 0x101170117177full>;
+
 // ------------------------------------------------------------------------------ per-lane context
-template <int N, int R, bool PAC, bool FULL>
+template <int N, int R, bool PAC, bool FULL, class SP>
 struct Ctx {
     static constexpr int NW = (N + 31) / 32;
     float lv[2 * R];      // register LLR levels: level d (2^d <= R) at lv[2^d .. 2^(d+1))
@@ -130,8 +153,8 @@ __device__ __forceinline__ float lds_rd8(const char* lds, uint32_t byte) {
 }
 
 // ------------------------------------------------------------------------------ leaf
-template <int N, int R, bool PAC, bool FULL, int I>
-__device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL>& c, float v) {
+template <int N, int R, bool PAC, bool FULL, class SP, int I>
+__device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL, SP>& c, float v) {
     if constexpr (FULL) {
         if (c.flags & kLeaf) {
             if constexpr (R == N) lds_wr(c.lds, c.leaf_row + 4 * I, v);
@@ -140,36 +163,36 @@ __device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL>& c, float v) {
     }
 }
 
-template <int N, int R, bool PAC, bool FULL, int I>
-__device__ __forceinline__ float genie(const Ctx<N, R, PAC, FULL>& c) {
+template <int N, int R, bool PAC, bool FULL, class SP, int I>
+__device__ __forceinline__ float genie(const Ctx<N, R, PAC, FULL, SP>& c) {
     if constexpr (R == N) return lds_rd(c.lds, c.gt_row + 4 * I);
     else return c.gt_g[I];
 }
 
-template <int N, int R, bool PAC, bool FULL, int I>
-__device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a, float L) {
-    const bool frozen = (c.fz[I >> 5] >> (I & 31)) & 1u;
+template <int N, int R, bool PAC, bool FULL, class SP, int I>
+__device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP>& c, const CodeParams& p, const Args& a, float L) {
+    const bool frozen = SP::on ? SP::frozen(I) : (((c.fz[I >> 5] >> (I & 31)) & 1u) != 0);
     const bool use_gt = FULL && (c.flags & kGt);
     float u;
     if constexpr (!PAC) {
         // polar.py:438/446: leaf = L + prior; prior = infty on frozen positions, 0 elsewhere
         const float lf = L + (frozen ? p.infty : 0.0f);
-        write_leaf<N, R, PAC, FULL, I>(c, lf);
-        u = use_gt ? genie<N, R, PAC, FULL, I>(c) : sgn_bits(lf);
+        write_leaf<N, R, PAC, FULL, SP, I>(c, lf);
+        u = use_gt ? genie<N, R, PAC, FULL, SP, I>(c) : sgn_bits(lf);
     } else {
-        write_leaf<N, R, PAC, FULL, I>(c, L);
+        write_leaf<N, R, PAC, FULL, SP, I>(c, L);
         const float u0 = (__builtin_popcount(c.st & p.tapmask) & 1) ? -1.0f : 1.0f;  // conv(+1) (pac_code.py:188-193)
         float v;
         if (frozen) {  // pac_code.py:545-551
             v = 1.0f;
             if (use_gt) {
-                u = genie<N, R, PAC, FULL, I>(c);
+                u = genie<N, R, PAC, FULL, SP, I>(c);
             } else {
                 u = u0;
                 c.st = (c.st << 1) & p.smask;
             }
         } else {  // pac_code.py:553-568, branch-free: u == u0 -> v = 1, u == -u0 -> v = -1, u == 0 -> v = 0
-            u = use_gt ? genie<N, R, PAC, FULL, I>(c) : sgn_bits(L);
+            u = use_gt ? genie<N, R, PAC, FULL, SP, I>(c) : sgn_bits(L);
             const bool eq = (u == u0), neg = (u == -u0);
             v = eq ? 1.0f : (neg ? -1.0f : 0.0f);
             const uint32_t sh = ((c.st << 1) | (neg ? 1u : 0u)) & p.smask;
@@ -185,19 +208,26 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL>& c, const CodeParams& 
 
 // ------------------------------------------------------------------------------ register levels
 // node at depth D (2^D <= R) covering absolute leaves [S0, S0 + 2^D); its LLRs at lv[2^D ..]
-template <int N, int R, bool PAC, bool FULL, int D, int S0>
-__device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a) {
+template <int N, int R, bool PAC, bool FULL, class SP, int D, int S0>
+__device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL, SP>& c, const CodeParams& p, const Args& a) {
     if constexpr (D == 0) {
-        leaf<N, R, PAC, FULL, S0>(c, p, a, c.lv[1]);
+        leaf<N, R, PAC, FULL, SP, S0>(c, p, a, c.lv[1]);
     } else {
         constexpr int h = 1 << (D - 1);
         constexpr int bs = S0 % R;  // local beta base
+        // a child whose leaves are all frozen needs no LLRs (msg-only PAC with a static frozen set)
+        constexpr bool skipL = SP::on && PAC && !FULL && SP::rate0(S0, h);
+        constexpr bool skipR = SP::on && PAC && !FULL && SP::rate0(S0 + h, h);
+        if constexpr (!skipL) {
 #pragma unroll
-        for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
-        node_reg<N, R, PAC, FULL, D - 1, S0>(c, p, a);
+            for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
+        }
+        node_reg<N, R, PAC, FULL, SP, D - 1, S0>(c, p, a);
+        if constexpr (!skipR) {
 #pragma unroll
-        for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[bs + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
-        node_reg<N, R, PAC, FULL, D - 1, S0 + h>(c, p, a);
+            for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[bs + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
+        }
+        node_reg<N, R, PAC, FULL, SP, D - 1, S0 + h>(c, p, a);
         if constexpr ((1 << D) < N) {  // the root's combined partial sums are never used
 #pragma unroll
             for (int j = 0; j < h; ++j) c.beta[bs + j] = c.beta[bs + j] * c.beta[bs + h + j];
@@ -206,8 +236,8 @@ __device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL>& c, const CodePara
 }
 
 // pack the float partial sums of a finished R-block starting at absolute position S0 into bits
-template <int N, int R, bool PAC, bool FULL, int S0>
-__device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL>& c) {
+template <int N, int R, bool PAC, bool FULL, class SP, int S0>
+__device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL, SP>& c) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int pos = S0 + j;
@@ -229,8 +259,8 @@ __device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL>& c) {
 
 // ------------------------------------------------------------------------------ upper levels
 // value j of the level-D LLR vector of the current node (D = n: staging input scaled; else LDS row)
-template <int N, int R, bool PAC, bool FULL, int D>
-__device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL>& c, const Args& a, int j) {
+template <int N, int R, bool PAC, bool FULL, class SP, int D>
+__device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL, SP>& c, const Args& a, int j) {
     (void)a;
     if constexpr ((1 << D) == N) {
         // staging: element j of the row is in chunk j/4, sub j%4
@@ -241,8 +271,8 @@ __device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL>& c, const Arg
     }
 }
 
-template <int N, int R, bool PAC, bool FULL, int D>
-__device__ __forceinline__ void up_put(Ctx<N, R, PAC, FULL>& c, int j, float v) {
+template <int N, int R, bool PAC, bool FULL, class SP, int D>
+__device__ __forceinline__ void up_put(Ctx<N, R, PAC, FULL, SP>& c, int j, float v) {
     if constexpr ((1 << D) == R) c.lv[R + j] = v;
     else lds_wr(c.lds, c.lvl_row[D] + 4 * j, v);
 }
@@ -267,11 +297,11 @@ __device__ __forceinline__ void stage_tile(char* lds, const Args& a, int64_t row
     }
 }
 
-template <int N, int R, bool PAC, bool FULL, int D, int S0>
-__device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParams& p, const Args& a) {
+template <int N, int R, bool PAC, bool FULL, class SP, int D, int S0>
+__device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP>& c, const CodeParams& p, const Args& a) {
     if constexpr ((1 << D) == R) {
-        node_reg<N, R, PAC, FULL, D, S0>(c, p, a);
-        pack_block<N, R, PAC, FULL, S0>(c);
+        node_reg<N, R, PAC, FULL, SP, D, S0>(c, p, a);
+        pack_block<N, R, PAC, FULL, SP, S0>(c);
     } else {
         constexpr int h = 1 << (D - 1);
         if constexpr ((1 << D) == N) {
@@ -280,17 +310,17 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
             for (int q = 0; q < h / 4; ++q) {
                 const float4 A = c.yrow[q];
                 const float4 Bv = c.yrow[q + h / 4];
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 0, f_minsum(rmul(c.scale, A.x), rmul(c.scale, Bv.x)));
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 1, f_minsum(rmul(c.scale, A.y), rmul(c.scale, Bv.y)));
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 2, f_minsum(rmul(c.scale, A.z), rmul(c.scale, Bv.z)));
-                up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + 3, f_minsum(rmul(c.scale, A.w), rmul(c.scale, Bv.w)));
+                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 0, f_minsum(rmul(c.scale, A.x), rmul(c.scale, Bv.x)));
+                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 1, f_minsum(rmul(c.scale, A.y), rmul(c.scale, Bv.y)));
+                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 2, f_minsum(rmul(c.scale, A.z), rmul(c.scale, Bv.z)));
+                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 3, f_minsum(rmul(c.scale, A.w), rmul(c.scale, Bv.w)));
             }
         } else {
 #pragma unroll
             for (int j = 0; j < h; ++j)
-                up_put<N, R, PAC, FULL, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, D>(c, a, j), up_get<N, R, PAC, FULL, D>(c, a, j + h)));
+                up_put<N, R, PAC, FULL, SP, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, SP, D>(c, a, j), up_get<N, R, PAC, FULL, SP, D>(c, a, j + h)));
         }
-        node_up<N, R, PAC, FULL, D - 1, S0>(c, p, a);
+        node_up<N, R, PAC, FULL, SP, D - 1, S0>(c, p, a);
         if constexpr ((1 << D) == N) {
             // second read of the row (L2 / MALL).  The pointer is laundered through an empty asm so the
             // compiler cannot forward the f step's loads: keeping those N values live across the left
@@ -306,7 +336,7 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int pos = S0 + 4 * q + e;
-                    up_put<N, R, PAC, FULL, D - 1>(c, 4 * q + e,
+                    up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + e,
                                              g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
                 }
             }
@@ -314,11 +344,11 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL>& c, const CodeParam
 #pragma unroll
             for (int j = 0; j < h; ++j) {
                 const int pos = S0 + j;
-                up_put<N, R, PAC, FULL, D - 1>(c, j, g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, up_get<N, R, PAC, FULL, D>(c, a, j),
-                                                      up_get<N, R, PAC, FULL, D>(c, a, j + h)));
+                up_put<N, R, PAC, FULL, SP, D - 1>(c, j, g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, up_get<N, R, PAC, FULL, SP, D>(c, a, j),
+                                                      up_get<N, R, PAC, FULL, SP, D>(c, a, j + h)));
             }
         }
-        node_up<N, R, PAC, FULL, D - 1, S0 + h>(c, p, a);
+        node_up<N, R, PAC, FULL, SP, D - 1, S0 + h>(c, p, a);
         if constexpr ((1 << D) < N) {
             // combine bit partial sums: left *= right  (h >= 64: whole words)
 #pragma unroll
@@ -362,7 +392,7 @@ __device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint3
 
 // ------------------------------------------------------------------------------ kernel
 // <= 256 VGPRs so two waves share each SIMD (N = 256 is LDS-bound at 3 waves per CU anyway)
-template <int N, int R, bool PAC, bool FULL>
+template <int N, int R, bool PAC, bool FULL, class SP>
 __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
@@ -370,7 +400,7 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
     constexpr int NP = Geo<N>::NP;
     const int lane = threadIdx.x;
 
-    Ctx<N, R, PAC, FULL> c;
+    Ctx<N, R, PAC, FULL, SP> c;
     c.lds = lds;
     c.scale = a.scale;
     c.flags = a.flags;
@@ -438,7 +468,7 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         // tile loop as 64-bit lane masks and spill them into VGPR lanes (two v_readlane per leaf, plus
         // scratch); an opaque per-tile copy keeps each test next to its leaf (one s_bitcmp).
 #pragma unroll
-        for (int w = 0; w < Ctx<N, R, PAC, FULL>::NW; ++w) {
+        for (int w = 0; w < Ctx<N, R, PAC, FULL, SP>::NW; ++w) {
             c.fz[w] = p.frozen[w];
             asm volatile("" : "+s"(c.fz[w]));
         }
@@ -452,9 +482,9 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
                 c.lv[N + 4 * q + 2] = rmul(c.scale, v.z);
                 c.lv[N + 4 * q + 3] = rmul(c.scale, v.w);
             }
-            node_reg<N, R, PAC, FULL, n, 0>(c, p, a);
+            node_reg<N, R, PAC, FULL, SP, n, 0>(c, p, a);
         } else {
-            node_up<N, R, PAC, FULL, n, 0>(c, p, a);
+            node_up<N, R, PAC, FULL, SP, n, 0>(c, p, a);
         }
 
         // ---- error counting against the Philox message stream (utils.py:17-51 semantics)
@@ -562,7 +592,7 @@ static Layout make_layout(bool pac, uint32_t flags) {
     return L;
 }
 
-template <int N, int R, bool PAC, bool FULL>
+template <int N, int R, bool PAC, bool FULL, class SP>
 static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
     const Layout L = make_layout<N, R>(PAC, a.flags);
     a.off_stage = L.off_stage;
@@ -573,7 +603,7 @@ static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
     a.off_info = L.off_info;
     a.off_lvl = L.off_lvl;
     a.ntiles = (a.B + kWave - 1) / kWave;
-    auto kern = sc_decode_kernel<N, R, PAC, FULL>;
+    auto kern = sc_decode_kernel<N, R, PAC, FULL, SP>;
     static bool attr_set[2] = {false, false};  // per instantiation; benign race (idempotent)
     if (!attr_set[0] && L.total > 65536) {
         NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
@@ -592,20 +622,36 @@ static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
 template <bool PAC, bool FULL>
 static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
     switch (p.N) {
-        case 4: return launch_t<4, 4, PAC, FULL>(p, a, s);
-        case 8: return launch_t<8, 8, PAC, FULL>(p, a, s);
-        case 16: return launch_t<16, 16, PAC, FULL>(p, a, s);
-        case 32: return launch_t<32, 32, PAC, FULL>(p, a, s);
-        case 64: return launch_t<64, 64, PAC, FULL>(p, a, s);
-        case 128: return launch_t<128, 64, PAC, FULL>(p, a, s);
-        case 256: return launch_t<256, 64, PAC, FULL>(p, a, s);
+        case 4: return launch_t<4, 4, PAC, FULL, NoSpec>(p, a, s);
+        case 8: return launch_t<8, 8, PAC, FULL, NoSpec>(p, a, s);
+        case 16: return launch_t<16, 16, PAC, FULL, NoSpec>(p, a, s);
+        case 32: return launch_t<32, 32, PAC, FULL, NoSpec>(p, a, s);
+        case 64: return launch_t<64, 64, PAC, FULL, NoSpec>(p, a, s);
+        case 128: return launch_t<128, 64, PAC, FULL, NoSpec>(p, a, s);
+        case 256: return launch_t<256, 64, PAC, FULL, NoSpec>(p, a, s);
         default: return fail(NPD_EINVAL, "sc_decode: unsupported N");
     }
+}
+
+static bool spec_off() {  // NPD_SC_NOSPEC=1: generic frozen set everywhere (testing / A-B); read per call
+    const char* e = getenv("NPD_SC_NOSPEC");
+    return e && e[0] == '1';
+}
+
+static bool is_frozen_set(const CodeParams& p, uint64_t m0, uint64_t m1) {
+    for (int i = 0; i < p.N; ++i) {
+        const bool f = ((p.frozen[i >> 5] >> (i & 31)) & 1u) != 0;
+        const bool g = (((i < 64) ? (m0 >> i) : (m1 >> (i - 64))) & 1ull) != 0;
+        if (f != g) return false;
+    }
+    return true;
 }
 
 static int run(const npd_code* code, Args a, hipStream_t s) {
     if (a.B == 0) return NPD_OK;
     const bool full = (a.flags & (kLeaf | kGt | kUhat)) != 0;
+    if (code->p.pac && !full && code->p.N == 128 && !spec_off() && is_frozen_set(code->p, 0x117177f177f7fffull, 0x101170117177full))
+        return launch_t<128, 64, true, false, SpecPacRm128>(code->p, a, s);
     if (code->p.pac) return full ? dispatch<true, true>(code->p, a, s) : dispatch<true, false>(code->p, a, s);
     return full ? dispatch<false, true>(code->p, a, s) : dispatch<false, false>(code->p, a, s);
 }

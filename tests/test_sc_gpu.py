@@ -179,6 +179,30 @@ def test_sc_decode_mc_counters_exact(oracle, N, K, pac):
         assert cnt.cpu().tolist() == [be, bl], (snr, cnt.cpu().tolist(), be, bl)
 
 
+def test_pac_static_frozen_set_kernel(monkeypatch, oracle):
+    """PAC(128,64) 'RM' msg-only decoding runs the kernel with the frozen set compiled in (rate-0 subtrees
+    decoded without LLRs); NPD_SC_NOSPEC=1 forces the run-time frozen set.  Identical msg_hat and counts, and
+    equal to the oracle, on noisy words plus crafted rows (zeros, huge and tiny magnitudes, constants)."""
+    code = pac_for(128, 64)
+    msg, _, y = code.mc_generate(3000 + 11, 1.0, 77, 0, 0)
+    rng = np.random.default_rng(3)
+    crafted = np.stack([np.zeros(128), np.full(128, 1e30), -np.full(128, 1e-30), rng.standard_normal(128) * 1e6,
+                        np.where(rng.random(128) < 0.5, 0.0, 1.0), np.full(128, -1.0)]).astype(np.float32)
+    y[: crafted.shape[0]] = torch.from_numpy(crafted).to(DEV)
+    out = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("NPD_SC_NOSPEC", env)
+        cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+        hat = torch.empty(y.shape[0], 64, device=DEV)
+        code.sc_decode_mc(y, 1.0, 77, 0, cnt, msg_hat=hat)
+        out.append((hat.cpu().numpy(), cnt.cpu().tolist()))
+    monkeypatch.delenv("NPD_SC_NOSPEC")
+    assert np.array_equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
+    _, oh, _ = oracle.pac_sc_decode(y.cpu().numpy(), 1.0, code.B)
+    assert np.array_equal(out[0][0], oh)
+
+
 def test_count_errors_golden():
     from neural_polar_decoder_amd import errors_ber, errors_bler
     d = golden("errors.npz")
