@@ -334,18 +334,19 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
     stream = torch.cuda.current_stream(dev)
     if do_sc:
         c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+        hat = torch.empty(B, 64, dtype=torch.float32, device=dev)  # decoded message bits, as the eval returns them
 
         def sc_step():
             for si, snr in enumerate(snrs):
-                code.sc_decode_mc(ys[si], snr, SEED, cw0, c[si])
+                code.sc_decode_mc(ys[si], snr, SEED, cw0, c[si], msg_hat=hat)
 
         t = timer(sc_step, iters=3, warm=1)
-        ms = event_ms(lambda: code.sc_decode_mc(ys[2], snrs[2], SEED, cw0, c[2]), 3, stream)
+        ms = event_ms(lambda: code.sc_decode_mc(ys[2], snrs[2], SEED, cw0, c[2], msg_hat=hat), 3, stream)
         c.zero_()
         sc_step()
         allreduce(c, _sum(), world)
         cc = c.cpu().numpy()
-        nb = 768 * B  # 4N + 4K bytes per codeword
+        nb = 768 * B  # 4N + 4K bytes per codeword: y in, msg_hat out
         out["pac_sc"] = {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
                          "avg_launch_ms": ms, "roofline": {"bound": "hbm", "achieved_gbs": nb / (ms / 1e3) / 1e9,
                                                            "peak_gbs": HBM_PEAK_GBS,
