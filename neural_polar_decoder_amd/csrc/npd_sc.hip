@@ -122,6 +122,7 @@ struct Ctx {
     float beta[R];        // partial sums of the current R-block
     uint32_t S[NW], Z[NW];  // sign / zero bits of partial sums of completed R-blocks (N > R only)
     uint32_t st;          // PAC conv state (bit t = 1 iff state[t] == -1)
+    int k;                // PAC: information leaves decided so far = slot of the next v decision
     uint32_t fz[NW];      // frozen-set words, re-read per tile (see the tile loop)
     // LDS row bases (bytes) of this lane
     char* lds;
@@ -199,7 +200,12 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP>& c, const CodePara
             c.st = (eq || neg) ? sh : c.st;
         }
         // v is read at information positions only (msg_hat, counts)
-        if (!frozen) lds_wr8(c.lds, c.v_row + I, v);
+        // v is read at information positions only (msg_hat, counts): stored in slot (message) order, so
+        // msg_hat leaves as 16-B rows
+        if (!frozen) {
+            lds_wr8(c.lds, c.v_row + (uint32_t)c.k, v);
+            ++c.k;
+        }
     }
     // u rows: every position for u_hat (FULL); Polar msg-only decoding needs information positions only
     if (FULL || (!PAC && !frozen)) lds_wr8(c.lds, c.u_row + I, u);
@@ -390,6 +396,24 @@ __device__ __forceinline__ void store_rows(const char* lds, uint32_t base, uint3
     }
 }
 
+// K int8 decisions per row in slot order -> fp32 msg_hat rows with 16-B stores (K % 4 == 0, 16-B aligned
+// output): one ds_read_b32 of 4 slots per float4
+__device__ __forceinline__ void store_slots(const char* lds, uint32_t base, uint32_t stride_b, int K, float* out,
+                                            int64_t tile_row0, int rows, int lane) {
+    const int K4 = K >> 2;
+    float4* dst = reinterpret_cast<float4*>(out + tile_row0 * (int64_t)K);
+    for (int e = lane; e < rows * K4; e += kWave) {
+        const int r = e / K4, c4 = e - r * K4;
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(lds + base + (uint32_t)r * stride_b + 4u * (uint32_t)c4);
+        float4 v;
+        v.x = (float)(int8_t)(w & 0xffu);
+        v.y = (float)(int8_t)((w >> 8) & 0xffu);
+        v.z = (float)(int8_t)((w >> 16) & 0xffu);
+        v.w = (float)(int8_t)(w >> 24);
+        dst[e] = v;
+    }
+}
+
 // ------------------------------------------------------------------------------ kernel
 // <= 256 VGPRs so two waves share each SIMD (N = 256 is LDS-bound at 3 waves per CU anyway)
 template <int N, int R, bool PAC, bool FULL, class SP>
@@ -429,6 +453,7 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
 
     uint32_t err_bits = 0, err_blocks = 0;
     const bool count = (a.flags & kCount) != 0;
+    const bool vec_msg = (p.K & 3) == 0 && (((uintptr_t)a.msg) & 15u) == 0;
 
     for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
         const int64_t row0 = t * kWave;
@@ -464,6 +489,7 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
         c.st = 0;
+        c.k = 0;
         // The frozen words are loop-invariant, so LICM would hoist all N per-leaf frozen tests out of the
         // tile loop as 64-bit lane masks and spill them into VGPR lanes (two v_readlane per leaf, plus
         // scratch); an opaque per-tile copy keeps each test next to its leaf (one s_bitcmp).
@@ -502,6 +528,22 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
                         const int k0 = blk * 128 + w * 32;
                         const int kn = (p.K - k0) < 32 ? (p.K - k0) : 32;
                         uint32_t bits = w4[w];
+                        if (PAC) {
+                            // slot-ordered v bytes, 4 per dword, against the message nibbles: +1 -> 0x01,
+                            // -1 -> 0xFF; a byte counts if it differs (0 decisions always do)
+                            for (int q = 0; q < kn; q += 4) {
+                                const uint32_t dw = *reinterpret_cast<const uint32_t*>(lds + dec_row + (uint32_t)(k0 + q));
+                                const uint32_t nib = (bits >> q) & 0xFu;
+                                const uint32_t x = (nib * 0x00204081u) & 0x01010101u;  // bit i -> byte i
+                                const uint32_t expect = 0x01010101u | ((x << 8) - x);
+                                const int valid = kn - q;
+                                const uint32_t vmask = valid >= 4 ? 0xFFFFFFFFu : ((1u << (8 * valid)) - 1u);
+                                const uint32_t d = (dw ^ expect) & vmask;
+                                const uint32_t tb = ((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d;
+                                e += (uint32_t)__builtin_popcount(tb & 0x80808080u);
+                            }
+                            continue;
+                        }
                         for (int j = 0; j < kn; ++j) {
                             const int pos = info_lds[k0 + j];  // wave-uniform LDS address: broadcast
                             const float u = lds_rd8(lds, dec_row + (uint32_t)pos);
@@ -519,8 +561,14 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         }
 
         // ---- coalesced output stores
-        if (a.flags & kMsg)
-            store_rows<true>(lds, PAC ? a.off_v : a.off_u, NB, info_lds, p.K, a.msg, row0, rows, lane);
+        if (a.flags & kMsg) {
+            if (PAC && vec_msg)
+                store_slots(lds, a.off_v, NB, p.K, a.msg, row0, rows, lane);
+            else if (PAC)
+                store_rows<true>(lds, a.off_v, NB, nullptr, p.K, a.msg, row0, rows, lane);
+            else
+                store_rows<true>(lds, a.off_u, NB, info_lds, p.K, a.msg, row0, rows, lane);
+        }
         if constexpr (FULL && R == N) {
             if (a.flags & kLeaf) store_rows<false>(lds, a.off_leaf, NP * 4, nullptr, N, a.leaf, row0, rows, lane);
         }
