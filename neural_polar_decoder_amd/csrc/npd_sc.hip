@@ -122,7 +122,7 @@ struct Ctx {
     float beta[R];        // partial sums of the current R-block
     uint32_t S[NW], Z[NW];  // sign / zero bits of partial sums of completed R-blocks (N > R only)
     uint32_t st;          // PAC conv state (bit t = 1 iff state[t] == -1)
-    int k;                // PAC: information leaves decided so far = slot of the next v decision
+    int k;                // information leaves decided so far = slot of the next msg decision (v for PAC)
     uint32_t fz[NW];      // frozen-set words, re-read per tile (see the tile loop)
     // LDS row bases (bytes) of this lane
     char* lds;
@@ -207,8 +207,14 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP>& c, const CodePara
             ++c.k;
         }
     }
-    // u rows: every position for u_hat (FULL); Polar msg-only decoding needs information positions only
-    if (FULL || (!PAC && !frozen)) lds_wr8(c.lds, c.u_row + I, u);
+    // PAC: u rows by position feed u_hat (FULL only).  Polar: the u decisions of information positions
+    // feed only msg_hat and the counts -> slot (message) order, like PAC's v rows
+    if constexpr (PAC) {
+        if (FULL) lds_wr8(c.lds, c.u_row + I, u);
+    } else if (!frozen) {
+        lds_wr8(c.lds, c.u_row + (uint32_t)c.k, u);
+        ++c.k;
+    }
     c.beta[I % R] = u;
 }
 
@@ -448,8 +454,6 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
             }
         }
     }
-    int32_t* info_lds = reinterpret_cast<int32_t*>(lds + a.off_info);
-    for (int k = lane; k < p.K; k += kWave) info_lds[k] = p.info[k];
 
     uint32_t err_bits = 0, err_blocks = 0;
     const bool count = (a.flags & kCount) != 0;
@@ -527,10 +531,10 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
                     for (int w = 0; w < 4; ++w) {
                         const int k0 = blk * 128 + w * 32;
                         const int kn = (p.K - k0) < 32 ? (p.K - k0) : 32;
-                        uint32_t bits = w4[w];
-                        if (PAC) {
-                            // slot-ordered v bytes, 4 per dword, against the message nibbles: +1 -> 0x01,
-                            // -1 -> 0xFF; a byte counts if it differs (0 decisions always do)
+                        const uint32_t bits = w4[w];
+                        {
+                            // slot-ordered decision bytes, 4 per dword, against the message nibbles: +1 ->
+                            // 0x01, -1 -> 0xFF; a byte counts if it differs (0 decisions always do)
                             for (int q = 0; q < kn; q += 4) {
                                 const uint32_t dw = *reinterpret_cast<const uint32_t*>(lds + dec_row + (uint32_t)(k0 + q));
                                 const uint32_t nib = (bits >> q) & 0xFu;
@@ -542,14 +546,6 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
                                 const uint32_t tb = ((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d;
                                 e += (uint32_t)__builtin_popcount(tb & 0x80808080u);
                             }
-                            continue;
-                        }
-                        for (int j = 0; j < kn; ++j) {
-                            const int pos = info_lds[k0 + j];  // wave-uniform LDS address: broadcast
-                            const float u = lds_rd8(lds, dec_row + (uint32_t)pos);
-                            const float m = (bits & 1u) ? -1.0f : 1.0f;
-                            bits >>= 1;
-                            e += (u != m) ? 1u : 0u;
                         }
                     }
                 }
@@ -562,12 +558,11 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
 
         // ---- coalesced output stores
         if (a.flags & kMsg) {
-            if (PAC && vec_msg)
-                store_slots(lds, a.off_v, NB, p.K, a.msg, row0, rows, lane);
-            else if (PAC)
-                store_rows<true>(lds, a.off_v, NB, nullptr, p.K, a.msg, row0, rows, lane);
+            const uint32_t slots = PAC ? a.off_v : a.off_u;  // decisions in message order
+            if (vec_msg)
+                store_slots(lds, slots, NB, p.K, a.msg, row0, rows, lane);
             else
-                store_rows<true>(lds, a.off_u, NB, info_lds, p.K, a.msg, row0, rows, lane);
+                store_rows<true>(lds, slots, NB, nullptr, p.K, a.msg, row0, rows, lane);
         }
         if constexpr (FULL && R == N) {
             if (a.flags & kLeaf) store_rows<false>(lds, a.off_leaf, NP * 4, nullptr, N, a.leaf, row0, rows, lane);
