@@ -726,6 +726,10 @@ static int launch(const CodeParams& p, Args a, hipStream_t s) {
     const size_t per_wave = (GEN ? (size_t)0 : (size_t)kWave * N * 4) + (size_t)kWave * NB;
     // as many waves per workgroup as fit (up to NPD_SCF_WPB): fewer workgroups -> fewer counter atomics
     int wpb = NPD_SCF_WPB;
+    if (const char* e = getenv("NPD_SCF_WPB")) {  // A/B: waves per workgroup (1..8)
+        const int v = atoi(e);
+        if (v >= 1 && v <= NPD_SCF_WPB) wpb = v;
+    }
     const size_t red = (size_t)8 * kMaxSeg;  // per wave: n_seg x {bits, blocks} uint32
     while (wpb > 1 && (size_t)wpb * (per_wave + red) + N > 160 * 1024) --wpb;
     const size_t lds = (size_t)wpb * (per_wave + red) + N;
