@@ -139,46 +139,64 @@ __global__ __launch_bounds__(256) void conv_layer_kernel(const float* __restrict
 
 // ------------------------------------------------------------------------------ FC GEMM
 // out[m][j] = act(sum_k X[m][k] * Wt[j][k] + bias[j]);  block tile 64 (m) x 64 (j), K step 32.
+// LDS rows of stride GK + 4 (16-B aligned; 32 rows read with ds_read_b128 at one k offset hit every bank
+// once per 16 lanes).  Within a K block, k-step s pairs k = s (lane half 0) with k = s + GK/2 (half 1),
+// so the A and B operands of 4 consecutive k-steps are one ds_read_b128 each (round 1: two ds_read_b32
+// per MFMA) and the tile lands in LDS with 16-B stores.
 constexpr int GK = 32;
-constexpr int GS = GK + 1;  // padded LDS row (floats): conflict-free column reads
+constexpr int GS = GK + 4;
 
 __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, const float* __restrict__ Wt,
                                                  const float* __restrict__ bias, float* __restrict__ out, int M, int K,
                                                  int Nout, int act) {
-    __shared__ float As[2][64 * GS];
-    __shared__ float Bs[2][64 * GS];
+    __shared__ __attribute__((aligned(16))) float As[2][64 * GS];
+    __shared__ __attribute__((aligned(16))) float Bs[2][64 * GS];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int m0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
     const int msub = wave & 1, jsub = wave >> 1;
     // loader mapping: 64 rows x 32 k = 512 float4 per operand; thread loads 2 float4 of A and of B
-    auto load = [&](int buf, int k0) {
+    f4 ra[2], rb[2];
+    auto fetch = [&](int k0) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int idx = tid + 256 * u;  // 0..511
             const int r = idx >> 3, c4 = (idx & 7) * 4;
             int mr = m0 + r;
             if (mr >= M) mr = M - 1;
-            const f4 a = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
-            const f4 w = *reinterpret_cast<const f4*>(Wt + (int64_t)(j0 + r) * K + k0 + c4);
-            float* as = &As[buf][r * GS + c4];
-            float* bs = &Bs[buf][r * GS + c4];
-            as[0] = a.x; as[1] = a.y; as[2] = a.z; as[3] = a.w;
-            bs[0] = w.x; bs[1] = w.y; bs[2] = w.z; bs[3] = w.w;
+            ra[u] = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
+            rb[u] = *reinterpret_cast<const f4*>(Wt + (int64_t)(j0 + r) * K + k0 + c4);
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            *reinterpret_cast<f4*>(&As[buf][r * GS + c4]) = ra[u];
+            *reinterpret_cast<f4*>(&Bs[buf][r * GS + c4]) = rb[u];
         }
     };
     f16v acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int nk = K / GK;
-    load(0, 0);
+    fetch(0);
+    stash(0);
     __syncthreads();
     for (int kb = 0; kb < nk; ++kb) {
         const int cur = kb & 1;
-        if (kb + 1 < nk) load(cur ^ 1, (kb + 1) * GK);
-        const float* as = &As[cur][(msub * 32 + col) * GS + h];
-        const float* bs = &Bs[cur][(jsub * 32 + col) * GS + h];
+        if (kb + 1 < nk) fetch((kb + 1) * GK);
+        const f4* as = reinterpret_cast<const f4*>(&As[cur][(msub * 32 + col) * GS + h * (GK / 2)]);
+        const f4* bs = reinterpret_cast<const f4*>(&Bs[cur][(jsub * 32 + col) * GS + h * (GK / 2)]);
 #pragma unroll
-        for (int s = 0; s < GK / 2; ++s) acc = mfma(as[2 * s], bs[2 * s], acc);
+        for (int g = 0; g < GK / 8; ++g) {
+            const f4 a = as[g], b = bs[g];
+            acc = mfma(a.x, b.x, acc);
+            acc = mfma(a.y, b.y, acc);
+            acc = mfma(a.z, b.z, acc);
+            acc = mfma(a.w, b.w, acc);
+        }
+        if (kb + 1 < nk) stash(cur ^ 1);
         __syncthreads();
     }
 #pragma unroll
