@@ -10,8 +10,10 @@ Secondary legs (same JSON line; every leg runs on every rank over its own codewo
 between barriers and reports the max over ranks; whole-job codewords/s):
   montecarlo      the Monte-Carlo step itself: Philox message -> encode -> AWGN -> SC -> count, all
                   SNR points, y never stored (fused kernel)
-  sc_plus_gru     the metric as named: the eval step of rnn_all.py:853-880 on the same words -- SC and
-                  CRISP GRU (hidden 64, 2 layers) both decode every word of the sweep (configs[1]+[2])
+  metric_as_named the metric as named (top-level record): the eval step of rnn_all.py:853-880 on the same
+                  words -- SC and CRISP GRU (hidden 64, 2 layers; trained with the reference's loop) both decode
+                  every word of the sweep (configs[1]+[2]); its own roofline (GRU kernel, fp32 MFMA) and
+                  cpu_baseline (oracle SC + GRU on the host cores)
   crisp_gru       configs[2]: GRU decode alone, B = 2^20, fp32 (plus opt-in bf16x3 / bf16 kernels)
   pac_gru         configs[3]: PAC(128,64) CRISP GRU, 2^20 codewords per GPU (2^23 at 8 GPUs), RCCL
                   all-reduce of the BER/BLER counters
@@ -60,6 +62,53 @@ def gru_flop_per_cw(N, F):
     return 2 * 3 * F * N + N * (2 * 3 * F * F + 2 * 2 * 3 * F * F + 2 * F)
 
 
+TRAINED_64_32 = os.path.join(ROOT, "tests", "golden", "trained_crisp_64_32.npz")
+
+
+def crisp_model(code, dev, precision="fp32"):
+    """The CRISP GRU (hidden 64, 2 layers, onehot y_input) of configs[2]: the Polar(64,32) decoder trained with
+    the reference's own training loop (tests/golden/gen_trained.py) when that fixture is present, else
+    PyTorch-default seeded weights.  Returns (net, decoder, description, fixture or None)."""
+    from neural_polar_decoder_amd.montecarlo import seeded_crisp
+    from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
+    if os.path.exists(TRAINED_64_32):
+        d = np.load(TRAINED_64_32)
+        N, F = int(d["N"]), int(d["F"])
+        net = RNN_Model("GRU", N + 2, F, 1, int(d["layers"]), N, 0, 0).to(dev).eval()
+        net.load_state_dict({k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w.")})
+        if not np.array_equal(d["info"], code.info_positions):
+            raise SystemExit("trained CRISP fixture is for another information set")
+        dec = RNN_decoder("y_input", N, code.info_positions, onehot=True, precision=precision)
+        return net, dec, "trained with the reference's training loop (tests/golden/trained_crisp_64_32.npz)", d
+    net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev, precision=precision)
+    return net, dec, "seeded untrained weights (trained fixture absent)", None
+
+
+def gru_vs_reference(fix, snrs, bit_err, blk_err, n_cw, K):
+    """GRU BER/BLER of this run against the reference's own Monte-Carlo curve for the same trained weights
+    (fixture: n words per SNR through RNN_decoder.decode on the CPU): two-sample z of BLER (binomial) and of
+    BER (per-codeword bit-error variance from the fixture's sum of squares)."""
+    if fix is None:
+        return None
+    out = {}
+    for i, s in enumerate(snrs):
+        j = [float(x) for x in fix["snr"]].index(float(s)) if float(s) in [float(x) for x in fix["snr"]] else None
+        if j is None:
+            continue
+        nr = int(fix["mc_n"])
+        pr, pb = int(fix["mc_blk_err"][j]) / nr, int(fix["mc_bit_err"][j]) / (nr * K)
+        p, b = blk_err[i] / n_cw, bit_err[i] / (n_cw * K)
+        pool = (int(fix["mc_blk_err"][j]) + blk_err[i]) / (nr + n_cw)
+        zb = (p - pr) / max(1e-300, np.sqrt(pool * (1 - pool) * (1 / nr + 1 / n_cw)))
+        ev = int(fix["mc_sq_err"][j]) / nr - (int(fix["mc_bit_err"][j]) / nr) ** 2   # var of bit errors per word
+        zr = (b - pb) * K / max(1e-300, np.sqrt(ev * (1 / nr + 1 / n_cw)))
+        out[str(s)] = {"ber": b, "ber_reference": pb, "z_ber": zr, "bler": p, "bler_reference": pr, "z_bler": zb}
+    out["reference_words_per_snr"] = int(fix["mc_n"])
+    out["within_4_sigma"] = bool(all(abs(v["z_ber"]) < 4 and abs(v["z_bler"]) < 4
+                                     for k, v in out.items() if isinstance(v, dict)))
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,7 +118,7 @@ def parse():
     ap.add_argument("--snrs", type=str, default="0,1,2,3,4")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gru", action="store_true", help="skip the GRU legs (sc_plus_gru, crisp_gru, pac_gru)")
+    ap.add_argument("--no-gru", action="store_true", help="skip the GRU legs (metric_as_named, crisp_gru, pac_gru)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--no-conv", action="store_true", help="skip the conv-model leg")
     ap.add_argument("--no-scl", action="store_true", help="skip the SC-List leg")
@@ -239,13 +288,13 @@ def mc_leg(code, snrs, B, cw0, world, timer, dev, ref_counts):
 
 
 def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
-    """The eval step the metric names (rnn_all.py:853-880): SC and CRISP GRU decode the same words at
-    every SNR point and both are counted."""
-    from neural_polar_decoder_amd.montecarlo import seeded_crisp
+    """The eval step the metric names (rnn_all.py:853-880): SC and the CRISP GRU decode the same words at every
+    SNR point and both are counted.  Its roofline is the GRU kernel's (fp32 MFMA; 99.8 % of the step)."""
     from neural_polar_decoder_amd.utils import count_errors
-    net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev)
+    net, dec, wdesc, fix = crisp_model(code, dev)
     c_sc = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     c_gru = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
 
     def step():
         code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)  # decoded_SC_msg_bits, rnn_all.py:853
@@ -253,27 +302,59 @@ def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
             count_errors(msg, dec.decode(net, False, yall[si]), c_gru[si], cols=code.info_positions)
 
     t = timer(step, iters=2, warm=1)
+    # the GRU kernel alone, HIP events on its stream (one launch = one SNR point's 2^20 words)
+    ms = event_ms(lambda: dec.decode(net, False, yall[2]), 3, stream)
     allreduce(c_gru, _sum(), world)
     n = 3 * world * B
     cg = c_gru.cpu().numpy()
+    flop_cw = gru_flop_per_cw(N_CODE, 64)
+    tf = flop_cw * B / (ms / 1e3) / 1e12
     return {"value": world * len(snrs) * B / t, "unit": "codewords/s (each decoded by SC and by the GRU)",
-            "ms_per_step": t * 1e3,
+            "ms_per_step": t * 1e3, "weights": wdesc,
+            "roofline": {"bound": "mfma", "kernel": "gru_decode_kernel<64,2,4> (fp32 v_mfma_f32_32x32x2_f32)",
+                         "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "frac": tf / FP32_PEAK_TF,
+                         "traffic": None, "algorithmic_flop_per_cw": flop_cw, "codewords_per_launch": B,
+                         "avg_launch_ms": ms},
             "gru_ber": {str(s): float(cg[i, 0]) / (n * K_CODE) for i, s in enumerate(snrs)},
             "gru_bler": {str(s): float(cg[i, 1]) / n for i, s in enumerate(snrs)},
+            "gru_vs_reference": gru_vs_reference(fix, snrs, cg[:, 0], cg[:, 1], n, K_CODE),
             "config": "configs[1]+[2]: Polar(64,32), 2^20 words per SNR per GPU, 0-4 dB; SC sweep launch + 5 CRISP "
-                      "GRU (hidden 64, 2 layers, fp32, seeded untrained weights) decodes + device counts"}
+                      "GRU (hidden 64, 2 layers, fp32) decodes + device counts"}
+
+
+def cpu_baseline_sc_gru(yall_host, snrs, info, net, budget_s):
+    """The metric-as-named step on the host: the oracle's SC (sc_decode) and GRU (gru_decode) restatements, C with
+    OpenMP on every core of the affinity set, decoding the same received words until ~budget_s of CPU work."""
+    from oracle import oracle as O
+    threads = available_cores()
+    O.set_num_threads(threads)
+    sd = {k: v.detach().float().cpu().numpy() for k, v in net.state_dict().items()}
+    nb = yall_host[0].shape[0]
+    O.gru_decode(yall_host[0][:256], sd, N_CODE, 64, 2, info)  # warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        for s, y in zip(snrs, yall_host):
+            O.sc_decode(y, s, info)
+            O.gru_decode(y, sd, N_CODE, 64, 2, info)
+            done += y.shape[0]
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "codewords/s (each decoded by SC and by the GRU)", "cores": threads,
+            "kind": "port", "sample": f"oracle sc_decode + gru_decode (C, OpenMP, {threads} threads): the first {nb} "
+                                      f"received words of each of {len(snrs)} SNR points, repeated ({done} codewords, "
+                                      f"{el:.1f} s)"}
 
 
 def gru_leg(code, dev, y, B, world, timer):
     """configs[2]: CRISP GRU hidden 64, 2 layers, Polar(64,32), B = 2^20, fused decode kernel.  The fp32
     kernel (the reference's arithmetic) is the value; the opt-in bf16x3 / bf16 MFMA kernels are timed
     beside it with their decision agreement against fp32 on the same words."""
-    from neural_polar_decoder_amd.montecarlo import seeded_crisp
     flop_cw = gru_flop_per_cw(N_CODE, 64)
     stream = torch.cuda.current_stream(dev)
     res, ref_dec = {}, None
     for prec, peak in (("fp32", FP32_PEAK_TF), ("bf16x3", 2516.6), ("bf16", 2516.6)):
-        net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev, precision=prec)
+        net, dec, wdesc, _ = crisp_model(code, dev, precision=prec)
         d0 = dec.decode(net, False, y)
         t = timer(lambda: dec.decode(net, False, y), iters=2, warm=0)
         ms = event_ms(lambda: dec.decode(net, False, y), 2, stream)
@@ -289,7 +370,7 @@ def gru_leg(code, dev, y, B, world, timer):
     return {"value": f["value"], "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": f["avg_launch_ms"],
             "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "algorithmic_flop_per_cw": flop_cw,
             "achieved_tflops": f["achieved_tflops"], "peak_tflops_fp32": FP32_PEAK_TF, "frac": f["frac"],
-            "bf16x3": res["bf16x3"], "bf16": res["bf16"],
+            "bf16x3": res["bf16x3"], "bf16": res["bf16"], "weights": wdesc,
             "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input, 2 dB, 2^20 per GPU"}
 
 
@@ -362,6 +443,7 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
             for si in range(len(snrs)):
                 count_errors(msg, dec.decode(net, False, ys[si]), c[si], cols=code.B)
 
+        dec.decode(net, False, ys[0][:64])  # weight packing + upload happen here, outside the timed region
         t = timer(gru_step, iters=1, warm=0)
         ms = event_ms(lambda: dec.decode(net, False, ys[2]), 1, stream)
         allreduce(c, _sum(), world)  # the RCCL BER reduce of configs[3]
@@ -580,8 +662,9 @@ def main():
         if world > 1:
             ref = allreduce(per_step_counts.to(dev), _sum(), world).cpu()
         legs["montecarlo"] = mc_leg(code, snrs, B, cw0, world, timer, dev, ref)
+    metric_as_named = None
     if not args.no_gru:
-        legs["sc_plus_gru"] = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat)
+        metric_as_named = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat)
         legs["crisp_gru"] = gru_leg(code, dev, ys[2], B, world, timer)
         legs["crisp_gru_f512"] = crisp_f512_leg(dev, rank, world, timer)
     if not (args.no_gru and args.no_pac):
@@ -610,7 +693,7 @@ def main():
         "data": "synthetic (Philox msg -> Plotkin encode -> AWGN), resident in HBM before timing",
         "config": {"workload": "configs[1]: Polar(N=64,K=32) min-sum SC decode + fused BER/BLER count, "
                                "batch 2^20 per SNR per GPU, SNR sweep 0-4 dB (the SC half of the metric; the "
-                               "SC + CRISP-GRU eval step is the sc_plus_gru leg)",
+                               "SC + CRISP-GRU eval step is the metric_as_named record)",
                    "code": "Polar(64,32) 'polar' rate profile", "batch_per_snr_per_gpu": B, "snr_db": snrs,
                    "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
         "world_size_rccl": world,
@@ -623,6 +706,8 @@ def main():
         "bler": {str(s): bler[s] for s in snrs},
         "ber_match": bool(ber_match),
     }
+    if metric_as_named is not None:
+        out["metric_as_named"] = metric_as_named
     out.update(legs)
     if not args.no_traffic and world == 1:
         traffic, how = pmc_traffic(args)
@@ -631,6 +716,11 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         ys_host = [y[: 1 << 18].cpu().numpy() for y in ys]
         out["cpu_baseline"] = cpu_baseline(ys_host, snrs, code.info_positions, args.cpu_seconds)
+        if metric_as_named is not None:
+            net, _, _, _ = crisp_model(code, dev)
+            yh = [y[:4096].cpu().numpy() for y in ys]
+            out["metric_as_named"]["cpu_baseline"] = cpu_baseline_sc_gru(yh, snrs, code.info_positions, net,
+                                                                         args.cpu_seconds)
     print(json.dumps(out), flush=True)
     return 0
 

@@ -205,6 +205,15 @@ int npd_count_errors(const float* ref, const float* hat, int64_t B, int K, unsig
 int npd_count_errors_cols(const float* ref, const float* hat, int64_t B, int K, int W, const int32_t* cols,
                           unsigned long long* counters, void* stream);
 
+/*
+ * errors_ber(ref, hat, mask) with an integer mask (utils.py:17-25; the loops pass torch.ones(...).long(),
+ * run_models.py:325-341): counters[0] += sum(mask * (round(ref) != round(hat))), counters[1] += sum(mask),
+ * over (B,K) arrays (mask int64).  errors_ber = counters[0] / counters[1], decided on the device (no host
+ * read of the mask).
+ */
+int npd_count_errors_masked(const float* ref, const float* hat, const int64_t* mask, int64_t B, int K,
+                            unsigned long long* counters, void* stream);
+
 /* ---------------------------------------------------------------------------------- CRISP GRU */
 /*
  * Create a GRU decoder from an RNN_Model state dict (rnn_all.py:294-398): nn.GRU(input_size, F,
@@ -238,6 +247,10 @@ int npd_conv_destroy(npd_conv* conv);
 int64_t npd_conv_workspace_bytes(const npd_conv* conv, int64_t B);
 int npd_conv_forward(const npd_conv* conv, const float* y, float* logits, float* decoded, void* workspace,
                      int64_t B, void* stream);
+/* As npd_conv_forward, and (if input4 != NULL) the intermediate activation convNet.forward also returns,
+ * input4 = layers3(input3) + input3 (models.py:750, :767), channels-first (B, embed/2, N) fp32. */
+int npd_conv_forward_ex(const npd_conv* conv, const float* y, float* logits, float* decoded, float* input4,
+                        void* workspace, int64_t B, void* stream);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,7 @@ SIGNATURES = [
     ("npd_list_prune_select", c_int, [c_void_p, c_int, c_int, c_void_p]),
     ("npd_count_errors", c_int, [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p]),
     ("npd_count_errors_cols", c_int, [c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    ("npd_count_errors_masked", c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p]),
     ("npd_gru_create", c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
     ("npd_gru_destroy", c_int, [c_void_p]),
     ("npd_gru_decode", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
@@ -56,6 +57,7 @@ SIGNATURES = [
     ("npd_conv_destroy", c_int, [c_void_p]),
     ("npd_conv_workspace_bytes", c_i64, [c_void_p, c_i64]),
     ("npd_conv_forward", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    ("npd_conv_forward_ex", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
 ]
 
 
@@ -94,6 +96,24 @@ def require_gpu(t: torch.Tensor, name: str):
         raise TypeError(f"{name} must be a torch.Tensor")
     if not t.is_cuda:
         raise NpdError(f"{name} must be a device (HIP) tensor: libnpd has no CPU path")
+
+
+def check_out(t, name: str, dtype: torch.dtype, numel: int, device: torch.device | None = None, optional=False):
+    """A caller-supplied output buffer the kernels write through a raw pointer: it must be a contiguous device
+    tensor of ``dtype`` with at least ``numel`` elements (on ``device``), or the kernel would write past it."""
+    if t is None:
+        if optional:
+            return
+        raise ValueError(f"{name} is required")
+    require_gpu(t, name)
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.numel() < numel:
+        raise ValueError(f"{name} holds {t.numel()} elements, the call writes {numel}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, the call runs on {device}")
 
 
 def compute_device() -> torch.device:

@@ -376,6 +376,27 @@ extern "C" int npd_conv_destroy(npd_conv* c) {
 
 static int64_t chunk_of(int64_t B) { return B < kChunk ? B : kChunk; }
 
+// input4 (models.py:750, returned by convNet.forward): the (nb, N, C) activation after layers3 (+ residual) as
+// the reference's channels-first (nb, C, N).  A 64 x 64 (position x channel) tile per workgroup through LDS,
+// so both the reads (channels contiguous) and the writes (positions contiguous) are coalesced.
+__global__ __launch_bounds__(256) void act_to_channels_first_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                    int N, int C) {
+    __shared__ float t[64][65];
+    const int64_t b = blockIdx.z;
+    const int l0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+    const float* src = in + b * (int64_t)N * C;
+    float* dst = out + b * (int64_t)N * C;
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int l = e >> 6, cc = e & 63;
+        if (l0 + l < N && c0 + cc < C) t[l][cc] = src[(int64_t)(l0 + l) * C + c0 + cc];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int cc = e >> 6, l = e & 63;
+        if (l0 + l < N && c0 + cc < C) dst[(int64_t)(c0 + cc) * N + l0 + l] = t[l][cc];
+    }
+}
+
 extern "C" int64_t npd_conv_workspace_bytes(const npd_conv* c, int64_t B) {
     if (!c || B <= 0) return 0;
     const int64_t Bc = chunk_of(B);
@@ -383,8 +404,16 @@ extern "C" int64_t npd_conv_workspace_bytes(const npd_conv* c, int64_t B) {
     return (3 * Bc * (int64_t)c->E * c->N + Bc * 4 * (int64_t)c->N + 2 * Bc * (int64_t)c->N) * 4 + 256;
 }
 
+extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* logits, float* decoded, float* input4,
+                                   void* workspace, int64_t B, void* stream);
+
 extern "C" int npd_conv_forward(const npd_conv* c, const float* y, float* logits, float* decoded, void* workspace,
                                 int64_t B, void* stream) {
+    return npd_conv_forward_ex(c, y, logits, decoded, nullptr, workspace, B, stream);
+}
+
+extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* logits, float* decoded, float* input4,
+                                   void* workspace, int64_t B, void* stream) {
     NPD_ARG(c != nullptr, "npd_conv_forward: conv is NULL");
     NPD_ARG(B >= 0, "npd_conv_forward: B < 0");
     if (B == 0) return NPD_OK;
@@ -438,6 +467,13 @@ extern "C" int npd_conv_forward(const npd_conv* c, const float* y, float* logits
             // block (i == 3, 5, 7) is the next block's input and residual
             if (i == 1 || i == 3 || i == 5 || i == 7) res_idx = out_idx;
             in_idx = out_idx;
+            if (i == 5 && input4) {  // input4 = layers3(input3) + residual3 (models.py:750)
+                dim3 gt((N + 63) / 64, (L.cout + 63) / 64, (unsigned)nb);
+                hipLaunchKernelGGL(act_to_channels_first_kernel, gt, dim3(256), 0, s, o, input4 + b0 * (int64_t)L.cout * N,
+                                   N, L.cout);
+                rc = launch_check("input4 transpose launch");
+                if (rc) return rc;
+            }
         }
         const float* flat = bufs[in_idx];  // (nb, N*E): l*E + c (FC0's weights are permuted to match)
         const int64_t K1 = (int64_t)E * N;

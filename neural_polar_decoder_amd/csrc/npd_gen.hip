@@ -250,6 +250,36 @@ __global__ __launch_bounds__(256) void count_errors_kernel(const CountArgs a) {
     if (threadIdx.x < 2 && red[threadIdx.x]) atomicAdd(a.counters + threadIdx.x, (unsigned long long)red[threadIdx.x]);
 }
 
+// Masked count (errors_ber's mask argument, utils.py:17-25): counters[0] += sum(mask * [round(ref) !=
+// round(hat)]), counters[1] += sum(mask), over (B, K) with an integer mask (the reference's loops pass
+// torch.ones(...).long(), run_models.py:325-326).  Both sums are exact (uint64); grid-stride over elements,
+// one atomic pair per workgroup.
+__global__ __launch_bounds__(256) void count_errors_masked_kernel(const float* __restrict__ ref,
+                                                                  const float* __restrict__ hat,
+                                                                  const int64_t* __restrict__ mask, int64_t n,
+                                                                  unsigned long long* counters) {
+    __shared__ unsigned long long red[2][4];
+    unsigned long long se = 0, sm = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const unsigned long long m = (unsigned long long)mask[i];
+        sm += m;
+        se += (rintf(ref[i]) != rintf(hat[i])) ? m : 0ull;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        se += __shfl_xor(se, o, 64);
+        sm += __shfl_xor(sm, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = se;
+        red[1][threadIdx.x >> 6] = sm;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+        if (v) atomicAdd(counters + threadIdx.x, v);
+    }
+}
+
 }  // namespace gen
 }  // namespace npd
 
@@ -362,4 +392,17 @@ extern "C" int npd_count_errors_cols(const float* ref, const float* hat, int64_t
     a.W = W;
     a.use_cols = 1;
     return count_launch(a, (hipStream_t)stream);
+}
+
+extern "C" int npd_count_errors_masked(const float* ref, const float* hat, const int64_t* mask, int64_t B, int K,
+                                       unsigned long long* counters, void* stream) {
+    NPD_ARG(B >= 0 && K >= 0, "npd_count_errors_masked: negative size");
+    NPD_ARG(counters != nullptr, "npd_count_errors_masked: counters is NULL");
+    if (B == 0 || K == 0) return NPD_OK;
+    NPD_ARG(ref != nullptr && hat != nullptr && mask != nullptr, "npd_count_errors_masked: null pointer");
+    const int64_t n = B * (int64_t)K;
+    const int grid = grid_for((n + 255) / 256, 4, device_cu_count());
+    hipLaunchKernelGGL(gen::count_errors_masked_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ref, hat, mask, n,
+                       counters);
+    return launch_check("count_errors_masked_kernel launch");
 }

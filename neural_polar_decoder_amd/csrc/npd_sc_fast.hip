@@ -21,28 +21,6 @@
 #ifndef NPD_SCF_WPB
 #define NPD_SCF_WPB 8  // waves per workgroup (each with its own LDS tile; they share only the counter reduction)
 #endif
-#ifndef NPD_SCF_NTS
-#define NPD_SCF_NTS 0  // non-temporal msg_hat stores
-#endif
-#ifndef NPD_SCF_NTL
-#define NPD_SCF_NTL 0  // non-temporal y loads
-#endif
-#ifndef NPD_SCF_BRANCHFREE
-#define NPD_SCF_BRANCHFREE 0
-#endif
-#ifndef NPD_SCF_ROOT_LDS
-#define NPD_SCF_ROOT_LDS 0  // 1: the root level is read from the LDS row image instead of 64 VGPRs
-#endif
-#ifndef NPD_SCF_PACKED
-#define NPD_SCF_PACKED 1  // g-updates and partial-sum products as packed fp32 pairs
-#endif
-#ifndef NPD_SCF_ABL
-#define NPD_SCF_ABL 0  // diagnostic builds only: 1 = skip the decode, 2 = skip the loads after the first tile,
-                       // 3 = loads + transposition only, 4 = loads only
-#endif
-#ifndef NPD_SCF_PREFETCH
-#define NPD_SCF_PREFETCH 1
-#endif
 
 namespace npd {
 namespace scf {
@@ -108,19 +86,10 @@ __device__ __forceinline__ void leaf(Lane<N>& c, const CodeParams& p, float L) {
     const uint32_t pbits = __builtin_amdgcn_readfirstlane(frozen ? fbits(c.infty) : 0u);
     const float lf = L + bitsf(pbits);  // polar.py:438/446
     const float u = sgn_bits(lf);                     // polar.py:479
-#if NPD_SCF_BRANCHFREE
-    // branch-free: frozen decisions go to the row's padding byte (NB - 1 >= N); one basic block, but
-    // the scheduler then keeps more values live (more VGPRs) -- measured slower at 2 waves/SIMD
-    constexpr uint32_t kPad = 4 * ((N / 4) | 1) - 1;
-    const uint32_t off = frozen ? kPad : c.slot;
-    *reinterpret_cast<int8_t*>(c.lds + c.u_row + off) = (int8_t)(int)u;
-    c.slot += frozen ? 0u : 1u;
-#else
     if (!frozen) {
         *reinterpret_cast<int8_t*>(c.lds + c.u_row + c.slot) = (int8_t)(int)u;
         ++c.slot;
     }
-#endif
     c.beta[I] = u;
 }
 
@@ -133,7 +102,7 @@ __device__ __forceinline__ void node(Lane<N>& c, const CodeParams& p) {
 #pragma unroll
         for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
         node<N, D - 1, S0>(c, p);
-        if constexpr (h >= 2 && NPD_SCF_PACKED) {
+        if constexpr (h >= 2) {
             // g and the partial-sum products as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth
             // per instruction).  u * a is exact (u in {-1, 0, 1}), so the fused form equals mul + add.
 #pragma unroll
@@ -151,7 +120,7 @@ __device__ __forceinline__ void node(Lane<N>& c, const CodeParams& p) {
         }
         node<N, D - 1, S0 + h>(c, p);
         if constexpr ((1 << D) < N) {
-            if constexpr (h >= 2 && NPD_SCF_PACKED) {
+            if constexpr (h >= 2) {
 #pragma unroll
                 for (int j = 0; j < h; j += 2) {
                     const f2 x = {c.beta[S0 + j], c.beta[S0 + j + 1]};
@@ -292,32 +261,6 @@ __device__ __forceinline__ uint32_t nz_bytes(uint32_t x) {
     return (uint32_t)__builtin_popcount(t & 0x80808080u);
 }
 
-// Root node with its input level (the received word, scaled) read from the lane's swizzled LDS row
-// twice -- for f and for g -- instead of being held in VGPRs across the whole left subtree.
-template <int N>
-__device__ __forceinline__ void root_lds(Lane<N>& c, const CodeParams& p, const char* lds, uint32_t row_chunk, int sw,
-                                         float scale) {
-    constexpr int C = N / 4, h = N / 2;
-    constexpr int n = log2c<N>();
-#pragma unroll
-    for (int q = 0; q < C / 2; ++q) {
-        const f4 A = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)(q ^ sw)));
-        const f4 Bv = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)((q + C / 2) ^ sw)));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) c.lv[h + 4 * q + e] = f_minsum(rmul(scale, A[e]), rmul(scale, Bv[e]));
-    }
-    node<N, n - 1, 0>(c, p);
-#pragma unroll
-    for (int q = 0; q < C / 2; ++q) {
-        const f4 A = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)(q ^ sw)));
-        const f4 Bv = *reinterpret_cast<const f4*>(lds + 16u * (row_chunk + (uint32_t)((q + C / 2) ^ sw)));
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            c.lv[h + 4 * q + e] = c.beta[4 * q + e] * rmul(scale, A[e]) + rmul(scale, Bv[e]);
-    }
-    node<N, n - 1, h>(c, p);
-}
-
 // msg_hat of one finished tile: its rows*K floats are contiguous in HBM; decisions are int8 in slot order
 template <int N>
 __device__ __forceinline__ void store_msg(const char* lds, uint32_t kU, float* msg, int64_t row0, int rows, int K,
@@ -350,11 +293,7 @@ __device__ __forceinline__ void store_msg(const char* lds, uint32_t kU, float* m
                     o.y = (float)(int8_t)((w[i] >> 8) & 0xFFu);
                     o.z = (float)(int8_t)((w[i] >> 16) & 0xFFu);
                     o.w = (float)(int8_t)(w[i] >> 24);
-#if NPD_SCF_NTS
-                    __builtin_nontemporal_store(o, reinterpret_cast<f4*>(dst + f));
-#else
                     *reinterpret_cast<f4*>(dst + f) = o;
-#endif
                 }
             }
         }
@@ -382,11 +321,7 @@ __device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4
     if ((t + 1) * kWave <= B) {
 #pragma unroll
         for (int q = 0; q < C; ++q) {
-#if NPD_SCF_NTL
-            nx[q] = __builtin_nontemporal_load(base + lane + kWave * q);
-#else
             nx[q] = base[lane + kWave * q];
-#endif
         }
     } else {
 #pragma unroll
@@ -397,19 +332,6 @@ __device__ __forceinline__ void load_tile(f4 (&nx)[C], const f4* __restrict__ y4
     }
 }
 
-#ifdef NPD_SCF_STAMPS
-// diagnostic build only: per-phase cycle sums per wave, written to counters + 2 (never in the product)
-#define STAMP(var)                                                                     \
-    do {                                                                               \
-        __builtin_amdgcn_sched_barrier(0);                                             \
-        unsigned long long _t;                                                         \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");    \
-        __builtin_amdgcn_sched_barrier(0);                                             \
-        var = _t;                                                                      \
-    } while (0)
-#else
-#define STAMP(var) do { } while (0)
-#endif
 template <int N>
 __device__ __forceinline__ void frozen_words_init(Lane<N>& c, const CodeParams& p) {
 #pragma unroll
@@ -519,10 +441,8 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
     int seg = (int)(g / (a.ntiles > 0 ? a.ntiles : 1));
     int64_t t = g - (int64_t)seg * a.ntiles;
     int cur_seg = seg;
-    if (!GEN && NPD_SCF_PREFETCH && g < total)
+    if (!GEN && g < total)
         load_tile<C>(nx, reinterpret_cast<const f4*>(a.y) + seg * segC, t, lane, a.B, segC - 1);
-    unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0;
-    unsigned long long ph[5] = {0, 0, 0, 0, 0};
     auto flush = [&](int sg) {
         const uint32_t eb = wave_sum_u32(err_bits);
         const uint32_t bl = wave_sum_u32(err_blocks);
@@ -534,14 +454,12 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
         err_blocks = 0;
     };
     for (; g < total; g += gstride) {
-        STAMP(ts0);
         if (a.count && seg != cur_seg) {
             flush(cur_seg);
             cur_seg = seg;
         }
         float scale = a.scale[seg];
         asm volatile("" : "+s"(scale));
-        const f4* y4 = reinterpret_cast<const f4*>(a.y) + seg * segC;
         const int64_t last4 = segC - 1;  // last valid float4 of this segment
         // next tile of this wave
         int64_t tn = t + gstride;
@@ -556,7 +474,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
         // The seed is made opaque per tile so the key schedule is recomputed with scalar adds here
         // instead of being hoisted into 20 loop-invariant SGPRs (which spill to VGPR lanes).
         uint32_t mw[4] = {0u, 0u, 0u, 0u};
-        if ((GEN || a.count) && NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4) {
+        if (GEN || a.count) {
             uint64_t sd = a.seed;
             asm volatile("" : "+s"(sd));
             const u32x4 o = philox_block(sd, kStreamMsg, a.cw_offset + (uint64_t)(row0 + lane), 0u);
@@ -565,7 +483,6 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
             mw[2] = o.z;
             mw[3] = o.w;
         }
-        STAMP(ts1);
         if constexpr (GEN && !SPEC) frozen_words_init(c, p);
         uint32_t Ubits[(N + 31) / 32];
         if constexpr (GEN) {
@@ -577,27 +494,21 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
             gen_llrs<N>(c.lv + N, Ubits, sd, kStreamNoise + a.snr_index0 + (uint32_t)seg, a.cw_offset + (uint64_t)(row0 + lane),
                         a.sigma[seg], scale);
         } else {
-        if (!NPD_SCF_PREFETCH) load_tile<C>(nx, y4, t, lane, a.B, last4);
         // ---- transpose the tile through LDS: chunk (lane + 64q) -> row r = (lane + 64q)/C, col chunk
 #pragma unroll
         for (int q = 0; q < C; ++q) {
             const int pch = lane + kWave * q;
             const int r = pch / C, cc = pch % C;
-            if (NPD_SCF_ABL == 4) {
-                if (nx[q].x == 123.f) *reinterpret_cast<f4*>(lds + kStage) = nx[q];
-            } else {
-                *reinterpret_cast<f4*>(lds + kStage + 16u * (uint32_t)(r * C + (cc ^ swz<C>(r)))) = nx[q];
-            }
+            *reinterpret_cast<f4*>(lds + kStage + 16u * (uint32_t)(r * C + (cc ^ swz<C>(r)))) = nx[q];
         }
         // ---- prefetch the next tile as soon as its registers are free (lands while this one is decoded)
-        if (NPD_SCF_PREFETCH && NPD_SCF_ABL != 2 && g + gstride < total)
+        if (g + gstride < total)
             load_tile<C>(nx, reinterpret_cast<const f4*>(a.y) + segn * segC, tn, lane, a.B, last4);
-        STAMP(ts2);
         // ---- previous tile's msg_hat (its decision rows are read before this tile's leaves overwrite them;
         // done before this tile's LLRs occupy registers)
-        if (NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4 && a.msg && pend_rows > 0)
+        if (a.msg && pend_rows > 0)
             store_msg<N>(lds, kU, a.msg + pend_seg * a.B * K, pend_row0, pend_rows, K, lane, NB);
-        if (!NPD_SCF_ROOT_LDS && NPD_SCF_ABL < 4) {
+        {
 #pragma unroll
             for (int q = 0; q < C; ++q) {
                 const f4 v = *reinterpret_cast<const f4*>(lds + kStage + 16u * (uint32_t)(lane * C + (q ^ sw)));
@@ -608,7 +519,6 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
             }
         }
         }  // !GEN
-        STAMP(ts3);
         // ---- decode.  The per-leaf frozen tests are loop-invariant; left alone the compiler hoists all
         // of them out of the tile loop and spills the resulting 64 SGPR pairs to VGPR lanes.  Making the
         // frozen words opaque per tile keeps each test a single s_bitcmp next to its leaf.
@@ -627,8 +537,7 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
             c.infty = inf;
         }
         c.slot = 0;
-        if constexpr (NPD_SCF_ABL == 1 || NPD_SCF_ABL == 3 || NPD_SCF_ABL == 4) {
-        } else if constexpr (SPEC) {
+        if constexpr (SPEC) {
             uint32_t bad = 0;
             spec::snode<N, MASK, n, 0>(c, bad);
             if (__ballot(bad != 0u) != 0ull) {
@@ -653,21 +562,18 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
                 frozen_words();
                 node<N, n, 0>(c, p);
             }
-        } else if (NPD_SCF_ROOT_LDS) {
-            root_lds<N>(c, p, lds + kStage, (uint32_t)(lane * C), sw, scale);
         } else {
             node<N, n, 0>(c, p);
         }
 
-        STAMP(ts4);
         // ---- error count: 4 slots per dword vs the Philox message bits (errors_ber/bler semantics)
-        if (a.count && NPD_SCF_ABL != 3 && NPD_SCF_ABL != 4) {
+        if (a.count) {
             // all decision dwords first (reads past slot K land in the next row or the slack after the last
             // wave's rows and are masked out), then branch-free masking: slots >= K contribute nothing
             uint32_t dec[N / 4];
 #pragma unroll
             for (int w = 0; w < N / 4; ++w)
-                dec[w] = NPD_SCF_ABL == 6 ? mw[1] : *reinterpret_cast<const uint32_t*>(lds + c.u_row + 4 * w);
+                dec[w] = *reinterpret_cast<const uint32_t*>(lds + c.u_row + 4 * w);
             uint32_t e = 0;
 #pragma unroll
             for (int w = 0; w < N / 4; ++w) {
@@ -685,28 +591,16 @@ __global__ __launch_bounds__(64 * NPD_SCF_WPB, GEN ? 2 : NPD_SCF_WPE * 4 / NPD_S
             }
         }
 
-        STAMP(ts5);
-        ph[0] += ts1 - ts0;  // message bits (Philox)
-        ph[1] += ts2 - ts1;  // wait for the tile, transposition writes, next prefetch issue
-        ph[2] += ts3 - ts2;  // previous tile's msg_hat stores, row reads
-        ph[3] += ts4 - ts3;  // SC decode
-        ph[4] += ts5 - ts4;  // error count
         pend_row0 = row0;
         pend_rows = rows;
         pend_seg = seg;
         seg = segn;
         t = tn;
     }
-#ifdef NPD_SCF_STAMPS
-    if (lane == 0 && a.counters) {
-        for (int i = 0; i < 5; ++i) atomicAdd(a.counters + 2 + i, ph[i]);
-        atomicAdd(a.counters + 7, 1ull);
-    }
-#endif
     // the last tile's msg_hat
     if (a.msg && pend_rows > 0) store_msg<N>(lds, kU, a.msg + pend_seg * a.B * K, pend_row0, pend_rows, K, lane, NB);
 
-    if (a.count && NPD_SCF_ABL != 5) {
+    if (a.count) {
         // one pair of device atomics per workgroup and segment: same-address atomics from every wave
         // serialise at the memory side (~20 us per launch at one pair per wave)
         flush(cur_seg);

@@ -82,7 +82,7 @@ class convNet(nn.Module):
         except Exception:
             pass
 
-    def logits(self, noisy_enc: torch.Tensor, want_decisions=True):
+    def logits(self, noisy_enc: torch.Tensor, want_decisions=True, want_input4=False):
         if self.training:
             raise _lib.NpdError("the fused convNet path is inference-only (eval mode)")
         y = _lib.f32c(_lib.stage(noisy_enc, "noisy_enc"))
@@ -95,17 +95,21 @@ class convNet(nn.Module):
         ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=y.device)
         lg = torch.empty(B, self.output_len, dtype=torch.float32, device=y.device)
         dec = torch.empty_like(lg) if want_decisions else None
-        _lib.check(L.npd_conv_forward(h, _lib.ptr(y), _lib.ptr(lg), _lib.ptr(dec), _lib.ptr(ws), B,
-                                      _lib.stream_of(y.device)), "npd_conv_forward")
+        in4 = torch.empty(B, self.hidden_dim // 2, self.output_len, dtype=torch.float32, device=y.device) \
+            if want_input4 else None
+        _lib.check(L.npd_conv_forward_ex(h, _lib.ptr(y), _lib.ptr(lg), _lib.ptr(dec), _lib.ptr(in4), _lib.ptr(ws), B,
+                                         _lib.stream_of(y.device)), "npd_conv_forward")
+        if want_input4:
+            return _lib.home(lg, noisy_enc), _lib.home(dec, noisy_enc), _lib.home(in4, noisy_enc)
         return _lib.home(lg, noisy_enc), _lib.home(dec, noisy_enc)
 
     def forward(self, noisy_enc, mask, trg_seq, device):
-        """models.py:742-767: returns (output, decoded_msg_bits, out_mask, logits, None); the
-        intermediate `input4` the reference also returns is not materialised by the fused kernels."""
-        lg, dec = self.logits(noisy_enc)
+        """models.py:742-767: returns (output, decoded_msg_bits, out_mask, logits, input4), input4 being the
+        (B, embed/2, N) activation after layers3 + residual, written out by the fused forward on request."""
+        lg, dec, in4 = self.logits(noisy_enc, want_input4=True)
         logits = lg.unsqueeze(-1)
         out = torch.sigmoid(logits)
-        return torch.cat((1 - out, out), -1), dec.unsqueeze(-1), mask, logits, None
+        return torch.cat((1 - out, out), -1), dec.unsqueeze(-1), mask, logits, in4
 
     def decode(self, noisy_enc, info_positions, mask, device, trg_seq=None):
         """models.py:769-772: (decoded_msg_bits (B,N,1), mask)."""

@@ -110,8 +110,10 @@ class SCMonteCarlo(MonteCarlo):
         super().__init__(code.K, snrs, total_cw, batch, seed, rank, world, device)
         self.code = code
         self._y = None
-        # Polar N <= 64: generation fused into the decode kernel (npd_sc_mc_sweep_fused), y never stored
-        self.fused = bool(fused) and hasattr(code, "sc_mc_sweep_fused") and code.N <= 64 and len(self.snrs) <= 16
+        # generation fused into the decode kernel (npd_sc_mc_sweep_fused), y never stored: the codes the fused
+        # kernels cover (code.fused_mc_supported, the same rule as the C ABI's)
+        self.fused = (bool(fused) and hasattr(code, "sc_mc_sweep_fused") and len(self.snrs) <= 16
+                      and getattr(code, "fused_mc_supported", lambda: False)())
 
     def count_batch(self, si, snr, cw_offset, n, counters_row):
         _, _, y = self.code.mc_generate(n, snr, self.seed, si, cw_offset, device=self.device, want_msg=False)
@@ -302,6 +304,15 @@ def _main(argv=None):
             net, dec, ccode = rnn_from_checkpoint(a.crisp_checkpoint)
             if ccode.N != a.N or ccode.K != a.K:
                 raise SystemExit("--crisp_checkpoint was trained for a different (N, K)")
+            # messages are generated and counted on `code`; the checkpoint's decoder reads its own info set
+            # (args.rate_profile), so the two codes must be the same code, not just the same (N, K)
+            cinfo = np.asarray(getattr(ccode, "info_positions", None) if a.code == "polar" else ccode.B)
+            info = np.asarray(code.info_positions if a.code == "polar" else code.B)
+            if not np.array_equal(np.sort(cinfo), np.sort(info)):
+                raise SystemExit("--crisp_checkpoint's information set (its rate profile) differs from the CLI code's "
+                                 "(--rate_profile/--target_K)")
+            if a.code == "pac" and getattr(ccode, "g", a.g) != a.g:
+                raise SystemExit("--crisp_checkpoint's PAC convolution polynomial differs from --g")
         else:
             net, dec = seeded_crisp(code, a.rnn_feature_size, a.rnn_depth, a.init_seed)
         crisp = GRUMonteCarlo(code, net, dec, snrs, a.test_size, a.batch_size, a.seed).run()

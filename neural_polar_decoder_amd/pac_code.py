@@ -147,8 +147,12 @@ class PAC:
 
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
-        y = _aligned(_lib.f32c(y))
+        if y.dim() != 2 or y.shape[1] != self.N:
+            raise ValueError(f"y must be (batch, {self.N}), got {tuple(y.shape)}")
         h = self._code_for(self.B)
+        _lib.check_out(counters, "counters", torch.int64, 2, y.device)
+        _lib.check_out(msg_hat, "msg_hat", torch.float32, y.shape[0] * h.K, y.device, optional=True)
+        y = _aligned(_lib.f32c(y))
         _lib.check(_lib.load().npd_sc_decode_mc(h.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(msg_hat), int(seed),
                                                 int(cw_offset), y.shape[0], _lib.ptr(counters), _lib.stream_of(y.device)),
                    "npd_sc_decode_mc")

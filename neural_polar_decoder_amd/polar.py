@@ -195,7 +195,11 @@ class PolarCode:
 
     def scl_decode_mc(self, y, snr, L, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
-        y = _aligned(y)
+        if y.dim() != 2 or y.shape[1] != self.N:
+            raise ValueError(f"y must be (batch, {self.N}), got {tuple(y.shape)}")
+        _lib.check_out(counters, "counters", torch.int64, 2, y.device)
+        _lib.check_out(msg_hat, "msg_hat", torch.float32, y.shape[0] * self.K, y.device, optional=True)
+        y = _aligned(_lib.f32c(y))
         _lib.check(_lib.load().npd_scl_decode_mc(self.code.h, _lib.ptr(y), llr_scale(snr), int(L), _lib.ptr(msg_hat),
                                                  int(seed), int(cw_offset), y.shape[0], _lib.ptr(counters),
                                                  _lib.stream_of(y.device)), "npd_scl_decode_mc")
@@ -283,10 +287,19 @@ class PolarCode:
                    "npd_mc_generate")
         return msg, x, y
 
+    def fused_mc_supported(self) -> bool:
+        """Codes whose Monte-Carlo step runs as one fused generate + decode + count launch
+        (npd_sc_mc_sweep_fused): Polar 8 <= N <= 64 with K <= 128."""
+        return 8 <= self.N <= 64 and self.K <= 128
+
     def sc_decode_mc_sweep(self, y, snrs, seed, cw_offset, counters, msg_hat=None):
         """y (n_snr, B, N) -> counters (n_snr, 2) += errors at each SNR, one launch (npd_sc_decode_mc_sweep)."""
         _lib.require_gpu(y, "y")
+        if y.dim() != 3 or y.shape[2] != self.N:
+            raise ValueError(f"y must be (n_snr, B, {self.N}), got {tuple(y.shape)}")
         n, B = y.shape[0], y.shape[1]
+        _lib.check_out(counters, "counters", torch.int64, 2 * n, y.device)
+        _lib.check_out(msg_hat, "msg_hat", torch.float32, n * B * self.K, y.device, optional=True)
         scales = np.asarray([llr_scale(s) for s in snrs], dtype=np.float32)
         if len(scales) != n:
             raise ValueError("one SNR per y segment")
@@ -300,8 +313,9 @@ class PolarCode:
     def sc_mc_sweep_fused(self, B, snrs, seed, cw_offset, counters, msg_hat=None, snr_index0=0):
         """counters (n_snr, 2) += errors of SC on B fresh codewords per SNR, generated in the decode kernel
         (npd_sc_mc_sweep_fused): identical counts to mc_generate(snr_index = snr_index0 + s) followed by
-        sc_decode_mc_sweep.  Polar codes, N <= 64."""
-        _lib.require_gpu(counters, "counters")
+        sc_decode_mc_sweep.  Codes with fused_mc_supported()."""
+        _lib.check_out(counters, "counters", torch.int64, 2 * len(snrs))
+        _lib.check_out(msg_hat, "msg_hat", torch.float32, len(snrs) * int(B) * self.K, counters.device, optional=True)
         sig = np.asarray([sigma_f32(s) for s in snrs], dtype=np.float32)
         scl = np.asarray([llr_scale(s) for s in snrs], dtype=np.float32)
         _lib.check(_lib.load().npd_sc_mc_sweep_fused(self.code.h, len(sig), sig.ctypes.data_as(ctypes.c_void_p),
@@ -312,6 +326,10 @@ class PolarCode:
 
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")
+        if y.dim() != 2 or y.shape[1] != self.N:
+            raise ValueError(f"y must be (batch, {self.N}), got {tuple(y.shape)}")
+        _lib.check_out(counters, "counters", torch.int64, 2, y.device)
+        _lib.check_out(msg_hat, "msg_hat", torch.float32, y.shape[0] * self.K, y.device, optional=True)
         y = _aligned(_lib.f32c(y))
         _lib.check(_lib.load().npd_sc_decode_mc(self.code.h, _lib.ptr(y), llr_scale(snr), _lib.ptr(msg_hat), int(seed),
                                                 int(cw_offset), y.shape[0], _lib.ptr(counters), _lib.stream_of(y.device)),

@@ -73,12 +73,24 @@ def errors_ber(y_true, y_pred, mask=None):
 
     Returns what the reference returns -- a float32 tensor of shape (1,) on ``y_true``'s device
     (``sum(sum(x)) / torch.sum(mask)``) -- so the eval loops' ``.item()`` works unchanged.  The count is
-    exact (device uint64) and divided in fp32 like the reference's float sums.  A mask with any entry
-    other than 1 takes the reference's formula, evaluated on the GPU."""
-    if mask is not None and not bool(torch.all(mask == 1)):
-        e, m = _masked_errors(y_true, y_pred, mask)
-        res = (e.sum() / torch.sum(m)).reshape(1).float()
-        return _lib.home(res, y_true)
+    exact (device uint64) and divided in fp32 like the reference's float sums.  An integer mask (the loops'
+    torch.ones(...).long()) is counted by npd_count_errors_masked -- sum(mask * err) / sum(mask), decided on
+    the device with no host read of the mask; a floating-point mask takes the reference's formula on the GPU."""
+    if mask is not None:
+        t = _lib.f32c(_lib.stage(y_true, "y_true"))
+        if mask.dtype.is_floating_point or mask.dtype.is_complex:
+            e, m = _masked_errors(y_true, y_pred, mask)
+            return _lib.home((e.sum() / torch.sum(m)).reshape(1).float(), y_true)
+        p = _lib.f32c(_lib.stage(y_pred, "y_pred", t.device))
+        m = _lib.stage(mask, "mask", t.device).to(torch.int64).contiguous()
+        t, p = t.reshape(t.shape[0], -1), p.reshape(p.shape[0], -1)
+        m = m.reshape(m.shape[0], -1)
+        if t.shape != p.shape or t.shape != m.shape:
+            raise ValueError(f"shape mismatch {tuple(t.shape)} / {tuple(p.shape)} / mask {tuple(m.shape)}")
+        c = torch.zeros(2, dtype=torch.int64, device=t.device)
+        _lib.check(_lib.load().npd_count_errors_masked(_lib.ptr(t), _lib.ptr(p), _lib.ptr(m), t.shape[0], t.shape[1],
+                                                       _lib.ptr(c), _lib.stream_of(t.device)), "npd_count_errors_masked")
+        return _lib.home((c[0:1].float() / c[1:2].float()), y_true)
     c = count_errors(y_true, y_pred)
     n = y_true.numel()
     res = c[0:1].float() / torch.tensor(float(n), dtype=torch.float32, device=c.device)

@@ -448,6 +448,8 @@ def gen_conv():
         logits = out[3].view(B, N).numpy()
         dec = out[1].view(B, N).numpy()
         extra = {"w." + k: v for k, v in sd.items()} if store_w else {}
+        if store_w:  # forward's fifth output, input4 = layers3(input3) + input3 (models.py:750, :767)
+            extra["input4"] = out[4].numpy()
         save(f"{name}.npz", y=y.numpy(), logits=logits, decoded=dec, embed=embed, N=N, seed=4242 + embed, **extra)
 
 

@@ -65,3 +65,26 @@ def test_conv_vs_oracle_ragged_batch(oracle):
     lg, dec = net.logits(torch.from_numpy(y).to(DEV))
     ref = oracle.conv_forward(y[::37], sd)
     check(lg.cpu().numpy()[::37], dec.cpu().numpy()[::37], ref)
+
+
+def test_conv_forward_returns_input4(oracle):
+    """convNet.forward's fifth output, input4 = layers3(input3) + input3 (models.py:750, :767), (B, embed/2, N):
+    against the reference's value (golden) and the float64 oracle, same 1e-5 bar as the logits (O(1) GELU
+    activations, dot products of <= 7 x 64 terms); the other outputs as decode/logits give them."""
+    d = golden("conv_small_64.npz")
+    sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    net = net_from(sd, int(d["embed"]), int(d["N"]))
+    y = torch.from_numpy(d["y"]).to(DEV)
+    out, dec, m, logits, in4 = net.forward(y, None, None, DEV)
+    assert in4.shape == d["input4"].shape and in4.is_cuda
+    assert np.abs(in4.cpu().numpy() - d["input4"]).max() < ATOL
+    _, o4 = oracle.conv_forward(d["y"], sd, want_input4=True)
+    assert np.abs(in4.cpu().numpy() - o4).max() < ATOL
+    check(logits.squeeze(-1).cpu().numpy(), dec.squeeze(-1).cpu().numpy(), d["logits"])
+    assert out.shape == (y.shape[0], int(d["N"]), 2)
+    # ragged batch over more than one 4096-codeword chunk
+    rng = np.random.default_rng(2)
+    yb = rng.standard_normal((4096 + 33, 64)).astype(np.float32)
+    _, _, b4 = net.logits(torch.from_numpy(yb).to(DEV), want_input4=True)
+    _, o4b = oracle.conv_forward(yb[::41], sd, want_input4=True)
+    assert np.abs(b4.cpu().numpy()[::41] - o4b).max() < ATOL

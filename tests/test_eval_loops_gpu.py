@@ -299,3 +299,25 @@ def test_counter_return_types_and_host_inputs():
     assert isinstance(b2, np.float64) and b2 == 0.5 and [int(i) for i in pos] == [0]
     m = torch.tensor([[1, 0, 1], [1, 1, 1]])
     assert errors_ber(t, p, mask=m).item() == 0.0
+
+
+@pytest.mark.parametrize("mask_kind", ["ones_long", "random_long", "bool", "float"])
+def test_errors_ber_masked_matches_reference_formula(mask_kind):
+    """errors_ber(..., mask) against utils.py:17-25's formula restated in plain torch on the CPU:
+    sum(sum(mask * ne(round(t), round(p)))) / sum(mask).  Integer masks go through npd_count_errors_masked
+    (decided on the device, no host read of the mask); float masks through the formula on the GPU."""
+    from neural_polar_decoder_amd import errors_ber
+    g = torch.Generator().manual_seed(5)
+    B, K = 3001, 32
+    t = 1.0 - 2.0 * (torch.rand(B, K, generator=g) < 0.5).float()
+    p = t.clone()
+    p[torch.rand(B, K, generator=g) < 0.03] *= -1
+    p[torch.rand(B, K, generator=g) < 0.01] = 0.0
+    m = {"ones_long": torch.ones(B, K).long(), "random_long": (torch.rand(B, K, generator=g) < 0.7).long(),
+         "bool": torch.rand(B, K, generator=g) < 0.5, "float": (torch.rand(B, K, generator=g) < 0.6).float()}[mask_kind]
+    x = (m.view(B, -1, 1) * torch.ne(torch.round(t.view(B, -1, 1)), torch.round(p.view(B, -1, 1)))).float()
+    want = (sum(sum(x)) / torch.sum(m)).item()
+    got = errors_ber(t.to(DEV), p.to(DEV), mask=m.to(DEV))
+    assert got.shape == (1,) and got.dtype == torch.float32 and got.is_cuda
+    assert got.item() == pytest.approx(want, rel=1e-6)
+    assert errors_ber(t, p, mask=m).item() == pytest.approx(want, rel=1e-6)  # host inputs staged

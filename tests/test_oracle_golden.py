@@ -72,8 +72,9 @@ def test_gru_oracle_golden(oracle, name):
 def test_conv_oracle_golden(oracle):
     d = golden("conv_small_64.npz")
     sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
-    lg = oracle.conv_forward(d["y"], sd)
+    lg, in4 = oracle.conv_forward(d["y"], sd, want_input4=True)
     assert np.abs(lg - d["logits"]).max() < 1e-5
+    assert np.abs(in4 - d["input4"]).max() < 1e-5  # forward's fifth output (models.py:750, :767)
 
 
 def test_conv_seed_generator_matches_golden_c5(oracle):
