@@ -35,6 +35,8 @@ enum Flags : uint32_t {
     kCount = 1u << 4,  // count errors against the Philox message stream
 };
 
+constexpr int kMaxSeg = 16;  // SNR points of one fused Monte-Carlo sweep launch
+
 struct Args {
     const float* y;
     float* leaf;
@@ -50,6 +52,13 @@ struct Args {
     uint32_t flags;
     // byte offsets inside the dynamic LDS block of the (single-wave) workgroup
     uint32_t off_stage, off_u, off_v, off_leaf, off_gt, off_info, off_lvl;
+    // segments: n_seg runs of B codewords decoded back to back (msg_hat and counters per segment).  GEN
+    // (fused Monte-Carlo sweep, npd_sc_mc_sweep_fused): segment s is generated in registers at seg_sigma[s] on
+    // noise stream kStreamNoise + snr_index0 + s and decoded with seg_scale[s]; y is not read.
+    int n_seg;
+    uint32_t snr_index0;
+    float seg_scale[kMaxSeg];
+    float seg_sigma[kMaxSeg];
 };
 
 // ------------------------------------------------------------------------------ small helpers
@@ -115,7 +124,7 @@ struct Spec {
 using SpecPacRm128 = Spec<0x117177f177f7fffull, 0x101170117177full>;
 
 // ------------------------------------------------------------------------------ per-lane context
-template <int N, int R, bool PAC, bool FULL, class SP>
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
 struct Ctx {
     static constexpr int NW = (N + 31) / 32;
     float lv[2 * R];      // register LLR levels: level d (2^d <= R) at lv[2^d .. 2^(d+1))
@@ -136,7 +145,98 @@ struct Ctx {
     float scale;
     uint32_t flags;
     const float4* yrow;   // N > R: this lane's received word in HBM (the root level is read from it directly)
+    // GEN: this lane's codeword bits (bit i set iff x_i = -1) and its noise stream
+    uint32_t U[NW];
+    uint64_t gseed, gcw;
+    uint32_t gstream;
+    float gsigma;
 };
+
+// GEN: chunk q (elements 4q .. 4q+3) of this lane's received word, value for value what npd_mc_generate writes
+// (npd_gen.hip): Philox noise block (cw, q) -> 4 Box-Muller normals -> y = x + fl32(sigma z)
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
+__device__ __forceinline__ float4 gen_chunk(const Ctx<N, R, PAC, FULL, SP, GEN>& c, uint64_t cw, int q) {
+    const u32x4 o = philox_block(c.gseed, c.gstream, cw, (uint32_t)q);
+    float z[4];
+    normals4(o, z);
+    const uint32_t bits = (c.U[(4 * q) >> 5] >> ((4 * q) & 31)) & 0xFu;
+    float4 y;
+    y.x = __fadd_rn((bits & 1u) ? -1.0f : 1.0f, __fmul_rn(c.gsigma, z[0]));
+    y.y = __fadd_rn((bits & 2u) ? -1.0f : 1.0f, __fmul_rn(c.gsigma, z[1]));
+    y.z = __fadd_rn((bits & 4u) ? -1.0f : 1.0f, __fmul_rn(c.gsigma, z[2]));
+    y.w = __fadd_rn((bits & 8u) ? -1.0f : 1.0f, __fmul_rn(c.gsigma, z[3]));
+    return y;
+}
+
+// GEN: message bits (Philox message block(s) of the codeword) -> v at the information positions -> PAC
+// convolution -> Plotkin transform, all on bit words (npd_gen.hip mc_generate_kernel, same bits)
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
+__device__ __forceinline__ void gen_codeword(Ctx<N, R, PAC, FULL, SP, GEN>& c, const CodeParams& p) {
+    constexpr int NW = Ctx<N, R, PAC, FULL, SP, GEN>::NW;
+    constexpr int MB = (N + 127) / 128;
+    uint32_t m[4 * MB];
+#pragma unroll
+    for (int blk = 0; blk < MB; ++blk) {
+        if (blk * 128 < p.K) {
+            const u32x4 o = philox_block(c.gseed, kStreamMsg, c.gcw, (uint32_t)blk);
+            m[4 * blk + 0] = o.x; m[4 * blk + 1] = o.y; m[4 * blk + 2] = o.z; m[4 * blk + 3] = o.w;
+        } else {
+            m[4 * blk + 0] = m[4 * blk + 1] = m[4 * blk + 2] = m[4 * blk + 3] = 0u;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) c.U[w] = 0u;
+    // scatter: the k-th information position (ascending) takes message bit k; the current message word is
+    // consumed by shifting (no run-time indexing into m), the next one selected every 32 bits
+    uint32_t cur = m[0];
+    int kk = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool frozen = SP::on ? SP::frozen(i) : (((c.fz[i >> 5] >> (i & 31)) & 1u) != 0);
+        if (!frozen) {
+            c.U[i >> 5] |= (cur & 1u) << (i & 31);
+            cur >>= 1;
+            ++kk;
+            if ((kk & 31) == 0) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int q = 1; q < 4 * MB; ++q) w = ((kk >> 5) == q) ? m[q] : w;
+                cur = w;
+            }
+        }
+    }
+    if constexpr (PAC) {
+        // u_i = v_i xor parity(state & taps), state bit t = v_{i-1-t} (pac_code.py:181-208): u = v xor the
+        // shifts of v by t + 1 for every tap t, on the whole bit vector (zeros shifted in = the +1 start state)
+        uint32_t v[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) v[w] = c.U[w];
+        uint32_t taps = p.tapmask;
+        asm volatile("" : "+s"(taps));
+        for (int t = 0; t < 31; ++t) {
+            if (!((taps >> t) & 1u)) continue;
+            const int sh = t + 1;
+#pragma unroll
+            for (int w = NW - 1; w >= 0; --w) {
+                const uint32_t lo = (w > 0) ? (v[w - 1] >> (32 - sh)) : 0u;
+                c.U[w] ^= (v[w] << sh) | (sh < 32 ? lo : 0u);
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 1; h < 32 && h < N; h <<= 1) {
+        uint32_t msk = 0;
+        for (int i = 0; i < 32; ++i)
+            if (((i / h) & 1) == 0) msk |= 1u << i;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) c.U[w] ^= (c.U[w] >> h) & msk;
+    }
+#pragma unroll
+    for (int hw = 1; hw < NW; hw <<= 1)
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if (((w / hw) & 1) == 0) c.U[w] ^= c.U[w + hw];
+}
 
 template <int N>
 __device__ __forceinline__ float4 stage_chunk(char* lds, uint32_t off_stage, uint32_t row_chunk, int sw, int c) {
@@ -154,8 +254,8 @@ __device__ __forceinline__ float lds_rd8(const char* lds, uint32_t byte) {
 }
 
 // ------------------------------------------------------------------------------ leaf
-template <int N, int R, bool PAC, bool FULL, class SP, int I>
-__device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL, SP>& c, float v) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int I>
+__device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL, SP, GEN>& c, float v) {
     if constexpr (FULL) {
         if (c.flags & kLeaf) {
             if constexpr (R == N) lds_wr(c.lds, c.leaf_row + 4 * I, v);
@@ -164,36 +264,36 @@ __device__ __forceinline__ void write_leaf(Ctx<N, R, PAC, FULL, SP>& c, float v)
     }
 }
 
-template <int N, int R, bool PAC, bool FULL, class SP, int I>
-__device__ __forceinline__ float genie(const Ctx<N, R, PAC, FULL, SP>& c) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int I>
+__device__ __forceinline__ float genie(const Ctx<N, R, PAC, FULL, SP, GEN>& c) {
     if constexpr (R == N) return lds_rd(c.lds, c.gt_row + 4 * I);
     else return c.gt_g[I];
 }
 
-template <int N, int R, bool PAC, bool FULL, class SP, int I>
-__device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP>& c, const CodeParams& p, const Args& a, float L) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int I>
+__device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP, GEN>& c, const CodeParams& p, const Args& a, float L) {
     const bool frozen = SP::on ? SP::frozen(I) : (((c.fz[I >> 5] >> (I & 31)) & 1u) != 0);
     const bool use_gt = FULL && (c.flags & kGt);
     float u;
     if constexpr (!PAC) {
         // polar.py:438/446: leaf = L + prior; prior = infty on frozen positions, 0 elsewhere
         const float lf = L + (frozen ? p.infty : 0.0f);
-        write_leaf<N, R, PAC, FULL, SP, I>(c, lf);
-        u = use_gt ? genie<N, R, PAC, FULL, SP, I>(c) : sgn_bits(lf);
+        write_leaf<N, R, PAC, FULL, SP, GEN, I>(c, lf);
+        u = use_gt ? genie<N, R, PAC, FULL, SP, GEN, I>(c) : sgn_bits(lf);
     } else {
-        write_leaf<N, R, PAC, FULL, SP, I>(c, L);
+        write_leaf<N, R, PAC, FULL, SP, GEN, I>(c, L);
         const float u0 = (__builtin_popcount(c.st & p.tapmask) & 1) ? -1.0f : 1.0f;  // conv(+1) (pac_code.py:188-193)
         float v;
         if (frozen) {  // pac_code.py:545-551
             v = 1.0f;
             if (use_gt) {
-                u = genie<N, R, PAC, FULL, SP, I>(c);
+                u = genie<N, R, PAC, FULL, SP, GEN, I>(c);
             } else {
                 u = u0;
                 c.st = (c.st << 1) & p.smask;
             }
         } else {  // pac_code.py:553-568, branch-free: u == u0 -> v = 1, u == -u0 -> v = -1, u == 0 -> v = 0
-            u = use_gt ? genie<N, R, PAC, FULL, SP, I>(c) : sgn_bits(L);
+            u = use_gt ? genie<N, R, PAC, FULL, SP, GEN, I>(c) : sgn_bits(L);
             const bool eq = (u == u0), neg = (u == -u0);
             v = eq ? 1.0f : (neg ? -1.0f : 0.0f);
             const uint32_t sh = ((c.st << 1) | (neg ? 1u : 0u)) & p.smask;
@@ -220,10 +320,10 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP>& c, const CodePara
 
 // ------------------------------------------------------------------------------ register levels
 // node at depth D (2^D <= R) covering absolute leaves [S0, S0 + 2^D); its LLRs at lv[2^D ..]
-template <int N, int R, bool PAC, bool FULL, class SP, int D, int S0>
-__device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL, SP>& c, const CodeParams& p, const Args& a) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int D, int S0>
+__device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL, SP, GEN>& c, const CodeParams& p, const Args& a) {
     if constexpr (D == 0) {
-        leaf<N, R, PAC, FULL, SP, S0>(c, p, a, c.lv[1]);
+        leaf<N, R, PAC, FULL, SP, GEN, S0>(c, p, a, c.lv[1]);
     } else {
         constexpr int h = 1 << (D - 1);
         constexpr int bs = S0 % R;  // local beta base
@@ -234,12 +334,12 @@ __device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL, SP>& c, const Code
 #pragma unroll
             for (int j = 0; j < h; ++j) c.lv[h + j] = f_minsum(c.lv[2 * h + j], c.lv[3 * h + j]);
         }
-        node_reg<N, R, PAC, FULL, SP, D - 1, S0>(c, p, a);
+        node_reg<N, R, PAC, FULL, SP, GEN, D - 1, S0>(c, p, a);
         if constexpr (!skipR) {
 #pragma unroll
             for (int j = 0; j < h; ++j) c.lv[h + j] = c.beta[bs + j] * c.lv[2 * h + j] + c.lv[3 * h + j];
         }
-        node_reg<N, R, PAC, FULL, SP, D - 1, S0 + h>(c, p, a);
+        node_reg<N, R, PAC, FULL, SP, GEN, D - 1, S0 + h>(c, p, a);
         if constexpr ((1 << D) < N) {  // the root's combined partial sums are never used
 #pragma unroll
             for (int j = 0; j < h; ++j) c.beta[bs + j] = c.beta[bs + j] * c.beta[bs + h + j];
@@ -248,8 +348,8 @@ __device__ __forceinline__ void node_reg(Ctx<N, R, PAC, FULL, SP>& c, const Code
 }
 
 // pack the float partial sums of a finished R-block starting at absolute position S0 into bits
-template <int N, int R, bool PAC, bool FULL, class SP, int S0>
-__device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL, SP>& c) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int S0>
+__device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL, SP, GEN>& c) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int pos = S0 + j;
@@ -271,8 +371,8 @@ __device__ __forceinline__ void pack_block(Ctx<N, R, PAC, FULL, SP>& c) {
 
 // ------------------------------------------------------------------------------ upper levels
 // value j of the level-D LLR vector of the current node (D = n: staging input scaled; else LDS row)
-template <int N, int R, bool PAC, bool FULL, class SP, int D>
-__device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL, SP>& c, const Args& a, int j) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int D>
+__device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL, SP, GEN>& c, const Args& a, int j) {
     (void)a;
     if constexpr ((1 << D) == N) {
         // staging: element j of the row is in chunk j/4, sub j%4
@@ -283,8 +383,8 @@ __device__ __forceinline__ float up_get(const Ctx<N, R, PAC, FULL, SP>& c, const
     }
 }
 
-template <int N, int R, bool PAC, bool FULL, class SP, int D>
-__device__ __forceinline__ void up_put(Ctx<N, R, PAC, FULL, SP>& c, int j, float v) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int D>
+__device__ __forceinline__ void up_put(Ctx<N, R, PAC, FULL, SP, GEN>& c, int j, float v) {
     if constexpr ((1 << D) == R) c.lv[R + j] = v;
     else lds_wr(c.lds, c.lvl_row[D] + 4 * j, v);
 }
@@ -309,46 +409,49 @@ __device__ __forceinline__ void stage_tile(char* lds, const Args& a, int64_t row
     }
 }
 
-template <int N, int R, bool PAC, bool FULL, class SP, int D, int S0>
-__device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP>& c, const CodeParams& p, const Args& a) {
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int D, int S0>
+__device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const CodeParams& p, const Args& a) {
     if constexpr ((1 << D) == R) {
-        node_reg<N, R, PAC, FULL, SP, D, S0>(c, p, a);
-        pack_block<N, R, PAC, FULL, SP, S0>(c);
+        node_reg<N, R, PAC, FULL, SP, GEN, D, S0>(c, p, a);
+        pack_block<N, R, PAC, FULL, SP, GEN, S0>(c);
     } else {
         constexpr int h = 1 << (D - 1);
         if constexpr ((1 << D) == N) {
-            // the root level straight from this lane's row in HBM (16-B loads)
+            // the root level straight from this lane's row in HBM (16-B loads), or generated (GEN)
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 A = c.yrow[q];
-                const float4 Bv = c.yrow[q + h / 4];
-                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 0, f_minsum(rmul(c.scale, A.x), rmul(c.scale, Bv.x)));
-                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 1, f_minsum(rmul(c.scale, A.y), rmul(c.scale, Bv.y)));
-                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 2, f_minsum(rmul(c.scale, A.z), rmul(c.scale, Bv.z)));
-                up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + 3, f_minsum(rmul(c.scale, A.w), rmul(c.scale, Bv.w)));
+                const float4 A = GEN ? gen_chunk(c, c.gcw, q) : c.yrow[q];
+                const float4 Bv = GEN ? gen_chunk(c, c.gcw, q + h / 4) : c.yrow[q + h / 4];
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 0, f_minsum(rmul(c.scale, A.x), rmul(c.scale, Bv.x)));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 1, f_minsum(rmul(c.scale, A.y), rmul(c.scale, Bv.y)));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 2, f_minsum(rmul(c.scale, A.z), rmul(c.scale, Bv.z)));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 3, f_minsum(rmul(c.scale, A.w), rmul(c.scale, Bv.w)));
             }
         } else {
 #pragma unroll
             for (int j = 0; j < h; ++j)
-                up_put<N, R, PAC, FULL, SP, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, SP, D>(c, a, j), up_get<N, R, PAC, FULL, SP, D>(c, a, j + h)));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j), up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j + h)));
         }
-        node_up<N, R, PAC, FULL, SP, D - 1, S0>(c, p, a);
+        node_up<N, R, PAC, FULL, SP, GEN, D - 1, S0>(c, p, a);
         if constexpr ((1 << D) == N) {
             // second read of the row (L2 / MALL).  The pointer is laundered through an empty asm so the
             // compiler cannot forward the f step's loads: keeping those N values live across the left
             // half would cost N VGPRs (N = 128: 384 instead of ~250 -> one wave per SIMD instead of two)
+            // (GEN: generated again, from a laundered codeword index so the f step's values are not kept live)
             const float4* yr = c.yrow;
             asm volatile("" : "+v"(yr));
+            uint64_t cw2 = c.gcw;
+            if constexpr (GEN) asm volatile("" : "+v"(cw2));
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 A = yr[q];
-                const float4 Bv = yr[q + h / 4];
+                const float4 A = GEN ? gen_chunk(c, cw2, q) : yr[q];
+                const float4 Bv = GEN ? gen_chunk(c, cw2, q + h / 4) : yr[q + h / 4];
                 const float av[4] = {A.x, A.y, A.z, A.w};
                 const float bv[4] = {Bv.x, Bv.y, Bv.z, Bv.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int pos = S0 + 4 * q + e;
-                    up_put<N, R, PAC, FULL, SP, D - 1>(c, 4 * q + e,
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + e,
                                              g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
                 }
             }
@@ -356,11 +459,11 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP>& c, const CodeP
 #pragma unroll
             for (int j = 0; j < h; ++j) {
                 const int pos = S0 + j;
-                up_put<N, R, PAC, FULL, SP, D - 1>(c, j, g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, up_get<N, R, PAC, FULL, SP, D>(c, a, j),
-                                                      up_get<N, R, PAC, FULL, SP, D>(c, a, j + h)));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j, g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j),
+                                                      up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j + h)));
             }
         }
-        node_up<N, R, PAC, FULL, SP, D - 1, S0 + h>(c, p, a);
+        node_up<N, R, PAC, FULL, SP, GEN, D - 1, S0 + h>(c, p, a);
         if constexpr ((1 << D) < N) {
             // combine bit partial sums: left *= right  (h >= 64: whole words)
 #pragma unroll
@@ -422,7 +525,7 @@ __device__ __forceinline__ void store_slots(const char* lds, uint32_t base, uint
 
 // ------------------------------------------------------------------------------ kernel
 // <= 256 VGPRs so two waves share each SIMD (N = 256 is LDS-bound at 3 waves per CU anyway)
-template <int N, int R, bool PAC, bool FULL, class SP>
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
 __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
@@ -430,7 +533,7 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
     constexpr int NP = Geo<N>::NP;
     const int lane = threadIdx.x;
 
-    Ctx<N, R, PAC, FULL, SP> c;
+    Ctx<N, R, PAC, FULL, SP, GEN> c;
     c.lds = lds;
     c.scale = a.scale;
     c.flags = a.flags;
@@ -459,14 +562,42 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
     const bool count = (a.flags & kCount) != 0;
     const bool vec_msg = (p.K & 3) == 0 && (((uintptr_t)a.msg) & 15u) == 0;
 
-    for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    // tiles of all segments: g = seg * ntiles + t (one segment unless a sweep / GEN launch)
+    const int64_t total = GEN ? a.ntiles * (int64_t)a.n_seg : a.ntiles;
+    int cur_seg = 0;
+    auto flush = [&](int sg) {
+        const uint32_t eb = wave_sum_u32(err_bits);
+        const uint32_t bl = wave_sum_u32(err_blocks);
+        if (lane == 0 && (eb | bl)) {
+            atomicAdd(a.counters + 2 * sg + 0, (unsigned long long)eb);
+            atomicAdd(a.counters + 2 * sg + 1, (unsigned long long)bl);
+        }
+        err_bits = 0;
+        err_blocks = 0;
+    };
+    for (int64_t g = blockIdx.x; g < total; g += gridDim.x) {
+        const int seg = GEN ? (int)(g / a.ntiles) : 0;
+        const int64_t t = GEN ? g - (int64_t)seg * a.ntiles : g;
         const int64_t row0 = t * kWave;
         const int rows = (int)((a.B - row0) < kWave ? (a.B - row0) : kWave);
+        if (GEN && count && seg != cur_seg) {
+            flush(cur_seg);
+            cur_seg = seg;
+        }
+        if constexpr (GEN) {
+            c.scale = a.seg_scale[seg];
+            c.gsigma = a.seg_sigma[seg];
+            c.gstream = kStreamNoise + a.snr_index0 + (uint32_t)seg;
+            c.gseed = a.seed;
+            // tail lanes decode a duplicate of the last codeword (not counted), as the streaming path does
+            c.gcw = a.cw_offset + (uint64_t)((row0 + lane) < a.B ? row0 + lane : a.B - 1);
+        }
 
         // ---- N <= R: stage the y tile through LDS (coalesced, transposed to row-per-lane).  N > R: each
         // lane reads the root level of its own row straight from HBM at the root's f and g steps (no LDS
         // stage: the LDS then holds only decision rows, so occupancy is register-bound)
-        if constexpr (R == N) {
+        if constexpr (GEN) {
+        } else if constexpr (R == N) {
             stage_tile<N>(lds, a, row0, lane);
         } else {
             const int64_t grow = (row0 + lane) < a.B ? row0 + lane : a.B - 1;
@@ -498,23 +629,24 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         // tile loop as 64-bit lane masks and spill them into VGPR lanes (two v_readlane per leaf, plus
         // scratch); an opaque per-tile copy keeps each test next to its leaf (one s_bitcmp).
 #pragma unroll
-        for (int w = 0; w < Ctx<N, R, PAC, FULL, SP>::NW; ++w) {
+        for (int w = 0; w < Ctx<N, R, PAC, FULL, SP, GEN>::NW; ++w) {
             c.fz[w] = p.frozen[w];
             asm volatile("" : "+s"(c.fz[w]));
         }
+        if constexpr (GEN) gen_codeword(c, p);
         if constexpr (R == N) {
-            // whole row into registers
+            // whole row into registers (GEN: generated in registers)
 #pragma unroll
             for (int q = 0; q < C; ++q) {
-                const float4 v = stage_chunk<N>(lds, a.off_stage, c.stage_row, c.sw, q);
+                const float4 v = GEN ? gen_chunk(c, c.gcw, q) : stage_chunk<N>(lds, a.off_stage, c.stage_row, c.sw, q);
                 c.lv[N + 4 * q + 0] = rmul(c.scale, v.x);
                 c.lv[N + 4 * q + 1] = rmul(c.scale, v.y);
                 c.lv[N + 4 * q + 2] = rmul(c.scale, v.z);
                 c.lv[N + 4 * q + 3] = rmul(c.scale, v.w);
             }
-            node_reg<N, R, PAC, FULL, SP, n, 0>(c, p, a);
+            node_reg<N, R, PAC, FULL, SP, GEN, n, 0>(c, p, a);
         } else {
-            node_up<N, R, PAC, FULL, SP, n, 0>(c, p, a);
+            node_up<N, R, PAC, FULL, SP, GEN, n, 0>(c, p, a);
         }
 
         // ---- error counting against the Philox message stream (utils.py:17-51 semantics)
@@ -559,10 +691,11 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         // ---- coalesced output stores
         if (a.flags & kMsg) {
             const uint32_t slots = PAC ? a.off_v : a.off_u;  // decisions in message order
+            float* msg = GEN ? a.msg + (int64_t)seg * a.B * p.K : a.msg;
             if (vec_msg)
-                store_slots(lds, slots, NB, p.K, a.msg, row0, rows, lane);
+                store_slots(lds, slots, NB, p.K, msg, row0, rows, lane);
             else
-                store_rows<true>(lds, slots, NB, nullptr, p.K, a.msg, row0, rows, lane);
+                store_rows<true>(lds, slots, NB, nullptr, p.K, msg, row0, rows, lane);
         }
         if constexpr (FULL && R == N) {
             if (a.flags & kLeaf) store_rows<false>(lds, a.off_leaf, NP * 4, nullptr, N, a.leaf, row0, rows, lane);
@@ -570,14 +703,7 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         if (FULL && (a.flags & kUhat)) store_rows<true>(lds, a.off_u, NB, nullptr, N, a.uhat, row0, rows, lane);
     }
 
-    if (count) {
-        const uint32_t eb = wave_sum_u32(err_bits);
-        const uint32_t bl = wave_sum_u32(err_blocks);
-        if (lane == 0) {
-            atomicAdd(a.counters + 0, (unsigned long long)eb);
-            atomicAdd(a.counters + 1, (unsigned long long)bl);
-        }
-    }
+    if (count) flush(cur_seg);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -635,7 +761,7 @@ static Layout make_layout(bool pac, uint32_t flags) {
     return L;
 }
 
-template <int N, int R, bool PAC, bool FULL, class SP>
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
 static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
     const Layout L = make_layout<N, R>(PAC, a.flags);
     a.off_stage = L.off_stage;
@@ -646,7 +772,8 @@ static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
     a.off_info = L.off_info;
     a.off_lvl = L.off_lvl;
     a.ntiles = (a.B + kWave - 1) / kWave;
-    auto kern = sc_decode_kernel<N, R, PAC, FULL, SP>;
+    if (!GEN || a.n_seg < 1) a.n_seg = 1;  // streaming launches decode one segment (y is one (B, N) block)
+    auto kern = sc_decode_kernel<N, R, PAC, FULL, SP, GEN>;
     static bool attr_set[2] = {false, false};  // per instantiation; benign race (idempotent)
     if (!attr_set[0] && L.total > 65536) {
         NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
@@ -657,21 +784,21 @@ static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
         (void)hipGetLastError();
         occ = 1;
     }
-    const int grid = grid_for(a.ntiles, occ, device_cu_count());
+    const int grid = grid_for(a.ntiles * a.n_seg, occ, device_cu_count());
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWave), L.total, stream, p, a);
     return launch_check("sc_decode_kernel launch");
 }
 
-template <bool PAC, bool FULL>
+template <bool PAC, bool FULL, bool GEN = false>
 static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
     switch (p.N) {
-        case 4: return launch_t<4, 4, PAC, FULL, NoSpec>(p, a, s);
-        case 8: return launch_t<8, 8, PAC, FULL, NoSpec>(p, a, s);
-        case 16: return launch_t<16, 16, PAC, FULL, NoSpec>(p, a, s);
-        case 32: return launch_t<32, 32, PAC, FULL, NoSpec>(p, a, s);
-        case 64: return launch_t<64, 64, PAC, FULL, NoSpec>(p, a, s);
-        case 128: return launch_t<128, 64, PAC, FULL, NoSpec>(p, a, s);
-        case 256: return launch_t<256, 64, PAC, FULL, NoSpec>(p, a, s);
+        case 4: return launch_t<4, 4, PAC, FULL, NoSpec, GEN>(p, a, s);
+        case 8: return launch_t<8, 8, PAC, FULL, NoSpec, GEN>(p, a, s);
+        case 16: return launch_t<16, 16, PAC, FULL, NoSpec, GEN>(p, a, s);
+        case 32: return launch_t<32, 32, PAC, FULL, NoSpec, GEN>(p, a, s);
+        case 64: return launch_t<64, 64, PAC, FULL, NoSpec, GEN>(p, a, s);
+        case 128: return launch_t<128, 64, PAC, FULL, NoSpec, GEN>(p, a, s);
+        case 256: return launch_t<256, 64, PAC, FULL, NoSpec, GEN>(p, a, s);
         default: return fail(NPD_EINVAL, "sc_decode: unsupported N");
     }
 }
@@ -694,9 +821,31 @@ static int run(const npd_code* code, Args a, hipStream_t s) {
     if (a.B == 0) return NPD_OK;
     const bool full = (a.flags & (kLeaf | kGt | kUhat)) != 0;
     if (code->p.pac && !full && code->p.N == 128 && !spec_off() && is_frozen_set(code->p, 0x117177f177f7fffull, 0x101170117177full))
-        return launch_t<128, 64, true, false, SpecPacRm128>(code->p, a, s);
+        return launch_t<128, 64, true, false, SpecPacRm128, false>(code->p, a, s);
     if (code->p.pac) return full ? dispatch<true, true>(code->p, a, s) : dispatch<true, false>(code->p, a, s);
     return full ? dispatch<false, true>(code->p, a, s) : dispatch<false, false>(code->p, a, s);
+}
+
+// fused Monte-Carlo sweep for every code the fast kernel does not take (PAC, Polar N >= 128, N = 4):
+// generation in registers, SC decode, counts (and msg_hat) per SNR segment, one launch
+static int gen_run(const npd_code* code, const float* sigma, const float* llr_scale, int n_seg, uint32_t snr_index0,
+                   float* msg, unsigned long long* counters, uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s) {
+    Args a{};
+    a.msg = msg;
+    a.counters = counters;
+    a.seed = seed;
+    a.cw_offset = cw_offset;
+    a.B = B;
+    a.n_seg = n_seg;
+    a.snr_index0 = snr_index0;
+    for (int i = 0; i < n_seg; ++i) {
+        a.seg_scale[i] = llr_scale[i];
+        a.seg_sigma[i] = sigma[i];
+    }
+    a.flags = (counters ? kCount : 0u) | (msg ? kMsg : 0u);
+    if (code->p.pac && code->p.N == 128 && !spec_off() && is_frozen_set(code->p, 0x117177f177f7fffull, 0x101170117177full))
+        return launch_t<128, 64, true, false, SpecPacRm128, true>(code->p, a, s);
+    return code->p.pac ? dispatch<true, false, true>(code->p, a, s) : dispatch<false, false, true>(code->p, a, s);
 }
 
 }  // namespace sc
@@ -798,6 +947,10 @@ extern "C" int npd_sc_mc_sweep_fused(const npd_code* code, int n_snr, const floa
     NPD_ARG(B >= 0, "npd_sc_mc_sweep_fused: B < 0");
     NPD_ARG(counters != nullptr || msg_hat != nullptr, "npd_sc_mc_sweep_fused: no output");
     if (B == 0) return NPD_OK;
-    return npd::sc_fast_run_gen(code->p, sigma, llr_scale, n_snr, snr_index0, msg_hat, counters, seed, cw_offset, B,
-                                (hipStream_t)stream);
+    const CodeParams& p = code->p;
+    if (!p.pac && p.N >= 8 && p.N <= 64 && p.K <= 128 && !fast_disabled())
+        return npd::sc_fast_run_gen(p, sigma, llr_scale, n_snr, snr_index0, msg_hat, counters, seed, cw_offset, B,
+                                    (hipStream_t)stream);
+    return sc::gen_run(code, sigma, llr_scale, n_snr, snr_index0, msg_hat, counters, seed, cw_offset, B,
+                       (hipStream_t)stream);
 }

@@ -18,6 +18,8 @@ import torch
 from . import _lib
 from .codes import pac_info_positions
 from .polar import _aligned, _CodeHandle, _Philox
+import ctypes
+
 from .utils import llr_scale, sigma_f32
 
 
@@ -144,6 +146,26 @@ class PAC:
                                                int(seed), int(snr_index), int(cw_offset), _lib.stream_of(device)),
                    "npd_mc_generate")
         return msg, x, y
+
+    def fused_mc_supported(self) -> bool:
+        """The PAC Monte-Carlo step runs as one fused generate + SC decode + count launch at every N."""
+        return 4 <= self.N <= 256
+
+    def sc_mc_sweep_fused(self, Bn, snrs, seed, cw_offset, counters, msg_hat=None, snr_index0=0):
+        """counters (n_snr, 2) += errors of PAC SC on Bn fresh codewords per SNR point, generated inside the
+        decode kernel (npd_sc_mc_sweep_fused; y never stored): identical counts and v_hat[:, B] to
+        mc_generate(snr_index = snr_index0 + s) followed by sc_decode_mc at each SNR (the configs[3] eval's
+        SC baseline, rnn_all.py:730-776, without the received words' HBM round trip)."""
+        h = self._code_for(self.B)
+        _lib.check_out(counters, "counters", torch.int64, 2 * len(snrs))
+        _lib.check_out(msg_hat, "msg_hat", torch.float32, len(snrs) * int(Bn) * h.K, counters.device, optional=True)
+        sig = np.asarray([sigma_f32(s) for s in snrs], dtype=np.float32)
+        scl = np.asarray([llr_scale(s) for s in snrs], dtype=np.float32)
+        _lib.check(_lib.load().npd_sc_mc_sweep_fused(h.h, len(sig), sig.ctypes.data_as(ctypes.c_void_p),
+                                                     scl.ctypes.data_as(ctypes.c_void_p), int(snr_index0), int(seed),
+                                                     int(cw_offset), int(Bn), _lib.ptr(msg_hat), _lib.ptr(counters),
+                                                     _lib.stream_of(counters.device)), "npd_sc_mc_sweep_fused")
+        return counters
 
     def sc_decode_mc(self, y, snr, seed, cw_offset, counters, msg_hat=None):
         _lib.require_gpu(y, "y")

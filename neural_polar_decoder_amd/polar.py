@@ -289,8 +289,8 @@ class PolarCode:
 
     def fused_mc_supported(self) -> bool:
         """Codes whose Monte-Carlo step runs as one fused generate + decode + count launch
-        (npd_sc_mc_sweep_fused): Polar 8 <= N <= 64 with K <= 128."""
-        return 8 <= self.N <= 64 and self.K <= 128
+        (npd_sc_mc_sweep_fused): every N the decoders compile (4 ... 256)."""
+        return 4 <= self.N <= 256
 
     def sc_decode_mc_sweep(self, y, snrs, seed, cw_offset, counters, msg_hat=None):
         """y (n_snr, B, N) -> counters (n_snr, 2) += errors at each SNR, one launch (npd_sc_decode_mc_sweep)."""
@@ -313,7 +313,7 @@ class PolarCode:
     def sc_mc_sweep_fused(self, B, snrs, seed, cw_offset, counters, msg_hat=None, snr_index0=0):
         """counters (n_snr, 2) += errors of SC on B fresh codewords per SNR, generated in the decode kernel
         (npd_sc_mc_sweep_fused): identical counts to mc_generate(snr_index = snr_index0 + s) followed by
-        sc_decode_mc_sweep.  Codes with fused_mc_supported()."""
+        sc_decode_mc_sweep.  Codes with fused_mc_supported(); at most 16 SNR points per call."""
         _lib.check_out(counters, "counters", torch.int64, 2 * len(snrs))
         _lib.check_out(msg_hat, "msg_hat", torch.float32, len(snrs) * int(B) * self.K, counters.device, optional=True)
         sig = np.asarray([sigma_f32(s) for s in snrs], dtype=np.float32)

@@ -98,3 +98,63 @@ def conv_weights_from_seed(embed, N, seed):
             arr = rng.uniform(-bnd, bnd, size=shape)
         sd[key] = arr.astype(np.float32)
     return sd
+
+
+def trained_fixture(name):
+    """A trained CRISP fixture (tests/golden/gen_trained.py) or a skip if it has not been generated."""
+    path = os.path.join(GOLDEN, name + ".npz")
+    if not os.path.exists(path):
+        pytest.skip(f"{name}.npz not generated (tests/golden/gen_trained.py)")
+    return np.load(path)
+
+
+def trained_words(d, si):
+    """The fixture's decision words at SNR index si, regenerated exactly as gen_trained.py drew them through
+    the reference (torch.manual_seed(seed_dec + si); msg = 1 - 2 (rand < 0.5); y = encode(msg) + sigma *
+    randn, polar.py:128-148, 201-207) -- the encoder is the oracle's (bit-exact +-1) -- and checked against
+    the stored sha256 of y.  Returns (msg (B,K), y (B,N)) as float32 numpy arrays."""
+    import hashlib
+    import torch
+    from oracle import oracle as O
+    N, K = int(d["N"]), int(d["K"])
+    torch.manual_seed(int(d["seed_dec"]) + si)
+    msg = 1.0 - 2.0 * (torch.rand(int(d["n_dec"]), K) < 0.5).float()
+    x = torch.from_numpy(O.encode_plotkin(msg.numpy(), N, d["info"]))
+    sigma = 10 ** (-float(d["snr"][si]) * 1.0 / 20)
+    y = x + sigma * torch.randn(x.shape, dtype=torch.float)
+    yn = y.numpy()
+    assert hashlib.sha256(np.ascontiguousarray(yn).tobytes()).hexdigest() == bytes(d[f"y_digest_{si}"]).decode(), \
+        "regenerated fixture words differ from the reference's (torch RNG stream changed?)"
+    return msg.numpy(), yn
+
+
+def trained_decisions(d, si):
+    """The reference's RNN_decoder.decode decisions at the information positions (+-1), (B, K)."""
+    K = int(d["K"])
+    bits = np.unpackbits(d[f"dec_bits_{si}"], axis=1)[:, :K]
+    return np.where(bits == 1, -1.0, 1.0).astype(np.float32)
+
+
+def db_offsets(snrs, bler, ref_snrs, ref_bler, min_bler=1e-4):
+    """Horizontal offset (dB) of a BLER curve from a reference curve: for each point, the SNR at which the
+    reference's log-BLER (linear in SNR between its grid points; the end segments extended linearly) equals
+    log(bler), minus the point's SNR.  Positive = the curve needs more SNR than the reference.  Points below
+    min_bler are skipped (None)."""
+    rs = np.asarray(ref_snrs, float)
+    lr = np.log(np.maximum(np.asarray(ref_bler, float), 1e-300))
+    out = []
+    for s, p in zip(snrs, bler):
+        if p < min_bler or p <= 0:
+            out.append(None)
+            continue
+        lp = np.log(p)
+        j = None
+        for i in range(len(rs) - 1):
+            if (lr[i] - lp) * (lr[i + 1] - lp) <= 0 and lr[i] != lr[i + 1]:
+                j = i
+                break
+        if j is None:  # outside the reference's range: the nearer end segment, extended
+            j = 0 if abs(lp - lr[0]) < abs(lp - lr[-1]) else len(rs) - 2
+        a, b = lr[j], lr[j + 1]
+        out.append(float(rs[j] + (lp - a) / (b - a) * (rs[j + 1] - rs[j]) - s))
+    return out

@@ -158,6 +158,37 @@ def gen_sc():
              gt_y=y.numpy(), gt=gt.numpy(), gt_snr=np.float64(1.0), gt_leaf=gleaf.numpy(), gt_msg_hat=ghat.numpy())
 
 
+def gen_sc_anchors():
+    """The reference's SC BER/BLER curve for Polar(64,32) (configs[1]) with enough words to resolve +-0.05 dB:
+    the eval loop's own draws (msg = 1 - 2 randint, encode_plotkin, channel, sc_decode_new; polar.py:128-148,
+    201-207, 465-484) in batches of 2^14, 2e5 words at 0-1 dB and 1e6 at 2-4 dB; error counts per SNR."""
+    import time
+    N, K = 64, 32
+    code = polar_code(N, K)
+    words = {0.0: 200_000, 1.0: 200_000, 2.0: 1_000_000, 3.0: 1_000_000, 4.0: 1_000_000}
+    nb = 1 << 14
+    out = {"snr": SNRS, "info": np.asarray(code.info_positions, np.int64)}
+    ns, bes, bls = [], [], []
+    for si, snr in enumerate(SNRS):
+        t0 = time.time()
+        be = bl = n = 0
+        b = 0
+        while n < words[float(snr)]:
+            m = min(nb, words[float(snr)] - n)
+            torch.manual_seed(90_000 + 1000 * si + b)
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (m, K)).float()
+            _, hat = code.sc_decode_new(code.channel(code.encode_plotkin(msg), float(snr)), float(snr))
+            e = (hat != msg).sum(1)
+            be += int(e.sum())
+            bl += int((e > 0).sum())
+            n += m
+            b += 1
+        ns.append(n); bes.append(be); bls.append(bl)
+        print(f"  {snr} dB: {n} words BER {be / (n * K):.4e} BLER {bl / n:.4e} ({time.time() - t0:.0f} s)", flush=True)
+    save("sc_anchors_64_32.npz", n=np.asarray(ns, np.int64), bit_err=np.asarray(bes, np.int64),
+         blk_err=np.asarray(bls, np.int64), **out)
+
+
 def tie_rows(N, rng, count):
     """Received words on a coarse grid: |LLR| values repeat, so list metrics tie at the pruning boundary
     and exact zeros occur -- pins torch.topk's tie rule and sign(0) paths."""

@@ -49,11 +49,11 @@ SNRS = [0.0, 1.0, 2.0, 3.0, 4.0]
 # name -> code, GRU and curriculum [(K, steps), ...] (run_crisp.sh style: K grows to the target)
 CASES = {
     "trained_crisp_32_16": dict(N=32, K=16, F=64, layers=2, snr_train=1.0, batch=4096, lr=1e-3,
-                                curriculum=[(4, 400), (8, 400), (12, 600), (16, 3000)],
+                                curriculum=[(4, 400), (8, 400), (12, 600), (16, 3000), (16, 6000)],
                                 n_dec=4096, n_logit=512, n_mc=1 << 20, n_sc=1 << 17, seed_dec=31, seed_mc=37),
     "trained_crisp_64_32": dict(N=64, K=32, F=64, layers=2, snr_train=1.0, batch=4096, lr=1e-3,
-                                curriculum=[(8, 500), (12, 500), (16, 500), (20, 500), (24, 600), (28, 800),
-                                            (32, 5000)],
+                                curriculum=[(8, 500), (12, 500), (16, 600), (20, 600), (24, 800), (28, 1000),
+                                            (32, 6000)],
                                 n_dec=4096, n_logit=256, n_mc=1 << 20, n_sc=1 << 16, seed_dec=41, seed_mc=43),
 }
 
@@ -67,8 +67,10 @@ def train(name, c, workdir):
     wd = os.path.join(workdir, name)
     os.makedirs(wd, exist_ok=True)
     prev = None
+    seen = {}
     for K, steps in c["curriculum"]:
-        path = os.path.join(wd, f"K{K}.pt")
+        seen[K] = seen.get(K, 0) + 1  # a K repeated in the curriculum continues from the previous stage
+        path = os.path.join(wd, f"K{K}.pt" if seen[K] == 1 else f"K{K}_{seen[K]}.pt")
         if os.path.exists(path) and os.path.exists(path + ".done"):
             if not os.path.exists(path + ".net"):
                 with torch.serialization.safe_globals([argparse.Namespace]):
@@ -200,8 +202,10 @@ def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     for name in args.cases:
         c = CASES[name]
-        ckpt = os.path.join(args.workdir, name, f"K{c['curriculum'][-1][0]}.pt") if args.eval_only else \
-            train(name, c, args.workdir)
+        lastK = c["curriculum"][-1][0]
+        nK = sum(1 for k, _ in c["curriculum"] if k == lastK)
+        ckpt = os.path.join(args.workdir, name, f"K{lastK}.pt" if nK == 1 else f"K{lastK}_{nK}.pt") \
+            if args.eval_only else train(name, c, args.workdir)
         evaluate(name, c, ckpt)
 
 

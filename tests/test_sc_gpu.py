@@ -235,25 +235,35 @@ def test_full_size_properties():
 
 
 def test_ber_curve_matches_reference_anchors():
-    """SC BER/BLER at 2^20 codewords/SNR vs the reference's anchors (BASELINE.md, 1e5 cw/SNR, torch RNG):
-    agreement within 4 combined standard errors (binomial, block-level for BER)."""
+    """SC BLER/BER at 2^22 codewords per SNR (fused Monte-Carlo, Philox words) vs the reference's own
+    sc_decode_new curve (tests/golden/sc_anchors_64_32.npz: 2e5 words at 0-1 dB, 1e6 at 2-4 dB, torch RNG):
+    within 4 two-sample standard errors (BLER binomial; BER with block-clustered bit errors bounded by the
+    block-level variance), and the BLER curve's horizontal offset from the reference's within +-0.05 dB at every
+    point (the north_star's BER-curve bar; standard error of the offset ~0.004-0.01 dB here)."""
+    from conftest import db_offsets
     from neural_polar_decoder_amd import reference_polar_code
-    anchors = {0: (1.944e-1, 5.664e-1), 1: (9.996e-2, 3.166e-1), 2: (3.634e-2, 1.248e-1),
-               3: (8.425e-3, 3.116e-2), 4: (1.258e-3, 4.910e-3)}
+    ref = golden("sc_anchors_64_32.npz")
+    snrs = [float(s) for s in ref["snr"]]
     code = reference_polar_code(64, 32)
-    B = 1 << 20
-    for si, (snr, (ber_ref, bler_ref)) in enumerate(anchors.items()):
-        _, _, y = code.mc_generate(B, float(snr), seed=1234, snr_index=si, cw_offset=0, want_msg=False)
-        cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
-        code.sc_decode_mc(y, float(snr), 1234, 0, cnt)
-        be, bl = cnt.cpu().tolist()
-        bler = bl / B
-        ber = be / (B * 32)
-        se_bler = np.sqrt(bler_ref * (1 - bler_ref) * (1 / 1e5 + 1 / B))
-        assert abs(bler - bler_ref) < 4 * se_bler + 1e-12, (snr, bler, bler_ref)
-        # bit errors cluster within blocks: bound with the block-level variance of errors per block
-        se_ber = np.sqrt((1 / 1e5 + 1 / B)) * np.sqrt(bler_ref) * (ber_ref / max(bler_ref, 1e-9)) * 2.5
-        assert abs(ber - ber_ref) < 4 * se_ber + 1e-12, (snr, ber, ber_ref)
+    B = 1 << 22
+    cnt = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    for off in range(0, B, 1 << 20):
+        code.sc_mc_sweep_fused(1 << 20, snrs, 1234, off, cnt)
+    c = cnt.cpu().numpy()
+    bler = []
+    for si, s in enumerate(snrs):
+        nr = int(ref["n"][si])
+        p, pr = c[si, 1] / B, int(ref["blk_err"][si]) / nr
+        ber, ber_r = c[si, 0] / (B * 32), int(ref["bit_err"][si]) / (nr * 32)
+        se = np.sqrt(pr * (1 - pr) * (1 / nr + 1 / B))
+        assert abs(p - pr) < 4 * se + 1e-12, (s, p, pr)
+        # bit errors per erroneous block <= K: Var(errors per word) <= K * E[errors per word]
+        se_ber = np.sqrt(32 * ber_r * 32 * (1 / nr + 1 / B)) / 32
+        assert abs(ber - ber_r) < 4 * se_ber + 1e-12, (s, ber, ber_r)
+        bler.append(p)
+    offs = db_offsets(snrs, bler, snrs, [int(x) / int(n) for x, n in zip(ref["blk_err"], ref["n"])])
+    for s, o in zip(snrs, offs):
+        assert o is not None and abs(o) <= 0.05, (s, o)
 
 
 def test_montecarlo_driver_shard_invariance():
@@ -311,45 +321,22 @@ def test_specialised_8_4_and_high_snr_vs_oracle(oracle):
             assert np.array_equal(code.sc_decode_msg(y, snr).cpu().numpy(), oh), (N, snr)
 
 
-@pytest.mark.parametrize("N,K,B", [(64, 32, 100_003), (32, 16, 5000), (16, 8, 777), (64, 22, 3001)])
-def test_sweep_equals_per_snr_calls(N, K, B):
-    """npd_sc_decode_mc_sweep (one launch over all SNR points) == separate npd_sc_decode_mc calls:
-    same msg_hat bits and counters at every SNR, ragged B, specialised and generic codes."""
-    from neural_polar_decoder_amd import PolarCode, reference_polar_code
-    from neural_polar_decoder_amd.codes import polar_info_positions
-    if K == 22:
-        info = polar_info_positions(N, K)
-        code = PolarCode(int(np.log2(N)), K, F=np.setdiff1d(np.arange(N), info))
-    else:
-        code = reference_polar_code(N, K)
-    snrs = [0.0, 1.5, 3.0, 5.0]
-    y = torch.empty(len(snrs), B, N, device=DEV)
-    for i, s in enumerate(snrs):
-        code.mc_generate(B, s, 11, i, 7, out=y[i], want_msg=False)
-    c1 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
-    h1 = torch.empty(len(snrs), B, K, device=DEV)
-    code.sc_decode_mc_sweep(y, snrs, 11, 7, c1, msg_hat=h1)
-    c2 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
-    for i, s in enumerate(snrs):
-        h = torch.empty(B, K, device=DEV)
-        code.sc_decode_mc(y[i], s, 11, 7, c2[i], msg_hat=h)
-        assert torch.equal(h, h1[i]), s
-    assert torch.equal(c1, c2)
-
-
-@pytest.mark.parametrize("N,K,B", [(64, 32, 100_003), (32, 16, 5000), (16, 8, 777), (64, 22, 3001), (8, 4, 4099)])
+@pytest.mark.parametrize("N,K,B", [(64, 32, 100_003), (32, 16, 5000), (16, 8, 777), (64, 22, 3001), (8, 4, 4099),
+                                   (4, 2, 1000), (128, 64, 20_001), (256, 128, 3333), (256, 200, 700)])
 def test_fused_mc_sweep_equals_generate_then_decode(N, K, B):
     """npd_sc_mc_sweep_fused (message -> codeword -> AWGN generated inside the decode kernel, y never
     stored) == npd_mc_generate + npd_sc_decode_mc_sweep: identical msg_hat and counters at every SNR,
     including 25 dB, where the specialised decoder's closed-form subtrees fall back to step-by-step SC
-    (regenerated received words)."""
+    (regenerated received words).  N <= 64: the fast kernel's GEN mode; N = 4, 128, 256: the generic
+    kernel's (K = 200 > 128: two Philox message blocks)."""
     from neural_polar_decoder_amd import PolarCode, reference_polar_code
     from neural_polar_decoder_amd.codes import polar_info_positions
-    if K == 22:
-        info = polar_info_positions(N, K)
+    if K in (22, 200):
+        info = polar_info_positions(N, K) if K == 22 else np.sort(np.random.default_rng(3).choice(N, K, replace=False))
         code = PolarCode(int(np.log2(N)), K, F=np.setdiff1d(np.arange(N), info))
     else:
         code = reference_polar_code(N, K)
+    assert code.fused_mc_supported()
     snrs = [-1.0, 1.5, 3.0, 25.0]
     seed, off, si0 = 13, 12345, 2
     y = torch.empty(len(snrs), B, N, device=DEV)
@@ -365,14 +352,46 @@ def test_fused_mc_sweep_equals_generate_then_decode(N, K, B):
     assert torch.equal(c1, c2), (c1.tolist(), c2.tolist())
 
 
-def test_fused_mc_rejects_unsupported_codes():
+@pytest.mark.parametrize("N,K,B,nospec", [(128, 64, 50_001, False), (128, 64, 3001, True), (64, 22, 4097, False),
+                                          (32, 16, 999, False), (256, 128, 2000, False)])
+def test_pac_fused_mc_sweep_equals_generate_then_decode(N, K, B, nospec, monkeypatch):
+    """PAC: the generic kernel's GEN mode (msg -> v -> convolution -> Plotkin -> AWGN in registers, PAC SC,
+    counts) == npd_mc_generate + npd_sc_decode_mc per SNR point: identical v_hat[:, B] and counters.
+    PAC(128,64) 'RM' runs the compile-time frozen-set kernel; nospec forces the run-time frozen set."""
     import argparse
-    from neural_polar_decoder_amd import PAC, NpdError, reference_polar_code
-    c = torch.zeros(1, 2, dtype=torch.int64, device=DEV)
+    from neural_polar_decoder_amd import PAC
+    if nospec:
+        monkeypatch.setenv("NPD_SC_NOSPEC", "1")
+    code = PAC(argparse.Namespace(target_K=K), N, K, 91)
+    assert code.fused_mc_supported()
+    snrs = [-1.0, 1.0, 2.5, 25.0]
+    seed, off, si0 = 29, 777, 1
+    c1 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    h1 = torch.empty(len(snrs), B, K, device=DEV)
+    for i, s in enumerate(snrs):
+        _, _, y = code.mc_generate(B, s, seed, si0 + i, off, device=DEV, want_msg=False)
+        code.sc_decode_mc(y, s, seed, off, c1[i], msg_hat=h1[i])
+    c2 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=DEV)
+    h2 = torch.empty(len(snrs), B, K, device=DEV)
+    code.sc_mc_sweep_fused(B, snrs, seed, off, c2, msg_hat=h2, snr_index0=si0)
+    assert torch.equal(h1, h2)
+    assert torch.equal(c1, c2), (c1.tolist(), c2.tolist())
+
+
+def test_fused_mc_argument_checks():
+    """Output buffers are validated before the kernel writes through their pointers; more than 16 SNR points
+    per call are refused by the C ABI."""
+    from neural_polar_decoder_amd import NpdError, reference_polar_code
+    code = reference_polar_code(64, 32)
+    with pytest.raises(ValueError):
+        code.sc_mc_sweep_fused(64, [1.0, 2.0], 1, 0, torch.zeros(1, 2, dtype=torch.int64, device=DEV))
+    with pytest.raises(TypeError):
+        code.sc_mc_sweep_fused(64, [1.0], 1, 0, torch.zeros(1, 2, dtype=torch.float32, device=DEV))
+    with pytest.raises(ValueError):
+        code.sc_mc_sweep_fused(64, [1.0], 1, 0, torch.zeros(1, 2, dtype=torch.int64, device=DEV),
+                               msg_hat=torch.empty(63, 32, device=DEV))
     with pytest.raises(NpdError):
-        reference_polar_code(128, 64).sc_mc_sweep_fused(64, [1.0], 1, 0, c)
-    pac = PAC(argparse.Namespace(target_K=64), 128, 64, 91)
-    assert not hasattr(pac, "sc_mc_sweep_fused")
+        code.sc_mc_sweep_fused(8, [1.0] * 17, 1, 0, torch.zeros(17, 2, dtype=torch.int64, device=DEV))
 
 
 def test_montecarlo_fused_equals_unfused():

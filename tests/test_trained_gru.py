@@ -1,0 +1,32 @@
+"""The oracle's GRU restatement at trained-model margins (CPU): decisions of oracle/ gru_decode on the trained
+fixture words (tests/golden/gen_trained.py: weights trained with the reference's own loop) against the
+reference's RNN_decoder.decode decisions, and its logits against the reference's.  Tolerance as for the
+seeded fixtures: logits within 2e-5 absolute on agreeing codewords; >= 99.9 % of information bits and
+>= 99 % of codewords identical."""
+import numpy as np
+import pytest
+
+from conftest import trained_decisions, trained_fixture, trained_words
+
+LOGIT_ATOL = 2e-5
+
+
+@pytest.mark.parametrize("name", ["trained_crisp_32_16", "trained_crisp_64_32"])
+def test_oracle_gru_trained_fixture(oracle, name):
+    d = trained_fixture(name)
+    N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
+    sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    info = d["info"]
+    for si in range(len(d["snr"])):
+        msg, y = trained_words(d, si)
+        n = 1024  # a CPU-sized slice of the 4096 words per SNR
+        dec, lg = oracle.gru_decode(y[:n], sd, N, F, L, info, onehot=True, want_logits=True)
+        ref = trained_decisions(d, si)[:n]
+        got = dec[:, info]
+        assert (got == ref).mean() >= 0.999
+        same = (got == ref).all(1)
+        assert same.mean() >= 0.99
+        m = min(n, d[f"logits_{si}"].shape[0])
+        assert np.abs(lg[:m][same[:m]] - d[f"logits_{si}"][:m][same[:m]]).max() < LOGIT_ATOL
+        # the net is trained: its confident logits are far from the untrained fixtures' near-zero values
+        assert np.median(np.abs(d[f"logits_{si}"][:, info])) > 0.1

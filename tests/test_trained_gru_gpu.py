@@ -1,0 +1,102 @@
+"""The fused CRISP GRU decoder (npd_gru_decode) at trained-model margins.
+
+Fixtures: tests/golden/trained_crisp_{32_16,64_32}.npz -- CRISP GRUs (hidden 64, 2 layers, onehot y_input)
+trained with the reference's own training loop (rnn_all.py run as-is over a K curriculum) by
+tests/golden/gen_trained.py, the reference's decisions and logits on 4096 words per SNR (0..4 dB) and its
+Monte-Carlo BER/BLER curve (2^20 words per SNR through RNN_decoder.decode on the CPU).
+
+Stated tolerance for the neural path (the north_star's "within a stated BER tolerance"):
+  (a) decisions on the fixture words: >= 99.9 % of information bits and >= 99 % of codewords identical to
+      the reference's; logits within 2e-5 absolute on codewords whose decisions agree (fp32, different
+      summation order);
+  (b) Monte-Carlo at 2^20 words per SNR (Philox words, independent of the reference's torch draws): BLER and
+      BER within 4 two-sample standard errors of the reference's curve (BLER binomial; BER with the
+      per-codeword bit-error variance from both sides), and the BLER curve's horizontal offset from the
+      reference's within +-0.05 dB at every point with BLER >= 1e-3 (standard error there ~0.01 dB).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import db_offsets, trained_decisions, trained_fixture, trained_words
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+LOGIT_ATOL = 2e-5
+CASES = ["trained_crisp_32_16", "trained_crisp_64_32"]
+
+
+def build(d):
+    from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
+    N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
+    net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).to(DEV).eval()
+    net.load_state_dict({k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w.")})
+    return net, RNN_decoder("y_input", N, d["info"], onehot=True)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_trained_gru_decisions_match_reference(name):
+    d = trained_fixture(name)
+    net, dec = build(d)
+    info = d["info"]
+    for si in range(len(d["snr"])):
+        _, y = trained_words(d, si)
+        out, lg = dec.decode(net, False, torch.from_numpy(y).to(DEV), return_logits=True)
+        got = out.cpu().numpy()[:, info]
+        ref = trained_decisions(d, si)
+        bits = (got == ref).mean()
+        same = (got == ref).all(1)
+        assert bits >= 0.999, (float(d["snr"][si]), bits)
+        assert same.mean() >= 0.99, (float(d["snr"][si]), same.mean())
+        m = d[f"logits_{si}"].shape[0]
+        err = np.abs(lg.cpu().numpy()[:m][same[:m]] - d[f"logits_{si}"][same[:m]]).max()
+        assert err < LOGIT_ATOL, (float(d["snr"][si]), err)
+
+
+def mc_counts(code, net, dec, snrs, n, seed, batch=1 << 18):
+    """bit errors, block errors and sum of squared per-codeword bit errors per SNR, HIP decoder on Philox
+    words (npd_mc_generate), counted on the device."""
+    info = torch.as_tensor(np.asarray(code.info_positions), device=DEV)
+    out = []
+    for si, s in enumerate(snrs):
+        be = bl = sq = 0
+        for off in range(0, n, batch):
+            m = min(batch, n - off)
+            msg, _, y = code.mc_generate(m, s, seed, si, off, device=DEV)
+            e = (dec.decode(net, False, y)[:, info] != msg).sum(1).to(torch.int64)
+            be += int(e.sum())
+            bl += int((e > 0).sum())
+            sq += int((e * e).sum())
+        out.append((be, bl, sq))
+    return out
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_trained_gru_ber_curve_matches_reference(name):
+    from neural_polar_decoder_amd import reference_polar_code
+    d = trained_fixture(name)
+    net, dec = build(d)
+    N, K = int(d["N"]), int(d["K"])
+    code = reference_polar_code(N, K)
+    assert np.array_equal(np.asarray(code.info_positions), d["info"])
+    snrs = [float(s) for s in d["snr"]]
+    n = 1 << 20
+    ours = mc_counts(code, net, dec, snrs, n, seed=2027)
+    nr = int(d["mc_n"])
+    bler = []
+    for si, s in enumerate(snrs):
+        be, bl, sq = ours[si]
+        rbe, rbl, rsq = int(d["mc_bit_err"][si]), int(d["mc_blk_err"][si]), int(d["mc_sq_err"][si])
+        p, pr = bl / n, rbl / nr
+        pool = (bl + rbl) / (n + nr)
+        z_bler = (p - pr) / np.sqrt(pool * (1 - pool) * (1 / n + 1 / nr))
+        v, vr = sq / n - (be / n) ** 2, rsq / nr - (rbe / nr) ** 2
+        z_ber = (be / n - rbe / nr) / np.sqrt(v / n + vr / nr)
+        assert abs(z_bler) < 4 and abs(z_ber) < 4, (s, p, pr, z_bler, be / (n * K), rbe / (nr * K), z_ber)
+        bler.append(p)
+    offs = db_offsets(snrs, bler, snrs, [int(x) / nr for x in d["mc_blk_err"]], min_bler=1e-3)
+    for s, o in zip(snrs, offs):
+        if o is not None:
+            assert abs(o) <= 0.05, (s, o)
+    # the trained decoder decodes: far below the coin-flip 0.5 of untrained weights at 2 dB
+    assert ours[2][0] / (n * K) < 0.4
