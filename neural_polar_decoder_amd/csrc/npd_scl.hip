@@ -465,11 +465,16 @@ static int launch_n(const CodeParams& p, const Args& a, hipStream_t s) {
 // read later (level D iff leaf i is in the left child of its level-D node) and the bit rows; all lanes
 // of the wave read element e before any lane writes it (one instruction stream), so copies between
 // lanes of a group need no double buffer.
+// N = 256: the top internal level (n-1, the root's two children, 128 values) is not stored but recomputed from y
+// (L1/L2) and the path's own partial-sum bits at the four steps that read it (leaves 0, N/4, N/2, 3N/4): 158
+// rows = 40 KB of LDS per wave instead of 73 KB, so four waves (one per SIMD) fit a CU instead of two; a path
+// switch then never copies that level either.
 template <int N>
 struct LdsRows {
     static constexpr int n = log2c<N>();
     static constexpr int W = N / 32;
-    static constexpr int kLv = N - 2;        // LLR rows
+    static constexpr bool kTopRec = N >= 256;
+    static constexpr int kLv = kTopRec ? N / 2 - 2 : N - 2;  // LLR rows (levels 1 .. n-1, or 1 .. n-2)
     static constexpr int kBS = kLv;          // beta sign words
     static constexpr int kBZ = kLv + W;      // beta zero words
     static constexpr int kDS = kLv + 2 * W;  // decision sign words
@@ -479,6 +484,25 @@ struct LdsRows {
 
 __device__ __forceinline__ float beta_val(uint32_t sw, uint32_t zw, int b) {
     return bitsf((((sw >> b) & 1u) << 31) | (((zw >> b) & 1u) ? 0u : 0x3f800000u));
+}
+
+// level n-1 of the tree (the root's left child if !right, else its right child), elements x .. x+3 of one
+// lane's path: f / g on the channel LLRs (polar.py:805-866 via updateLLR), g with the path's partial sums of
+// the root's left half (sign / zero bit words BS / BZ, positions 0 .. N/2-1)
+template <int N>
+__device__ __forceinline__ f4 top4(const f4* y4, float scale, int x, bool right, const uint32_t* BW, int rowBS,
+                                   int rowBZ, int lane) {
+    const f4 u = y4[x >> 2], v = y4[(x + N / 2) >> 2];
+    f4 o;
+    if (!right) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f_minsum(rmul(scale, u[e]), rmul(scale, v[e]));
+    } else {
+        const uint32_t sw = BW[(rowBS + (x >> 5)) * kWave + lane], zw = BW[(rowBZ + (x >> 5)) * kWave + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = beta_val(sw, zw, (x + e) & 31) * rmul(scale, u[e]) + rmul(scale, v[e]);
+    }
+    return o;
 }
 
 template <int N, int G>
@@ -513,7 +537,27 @@ __global__ __launch_bounds__(64) void scl_lds_kernel(const CodeParams p, const A
 
         for (int i = 0; i < N; ++i) {
             int d;  // level the f chain starts from
-            if (i == 0) {  // left child of the root: f on the channel LLRs
+            if (R::kTopRec && (i & (N / 4 - 1)) == 0) {
+                // level n-2 from the recomputed level n-1: f at leaves 0 and N/2 (left children), g at N/4 and 3N/4
+                constexpr int h2 = N / 4;
+                const bool right = i >= N / 2;
+                const bool gstep = (i & (N / 2 - 1)) != 0;
+                const int s0 = i - h2;  // g: the left sibling's partial sums are bits s0 .. s0 + h2 - 1
+                for (int q = 0; q < h2 / 4; ++q) {
+                    const f4 A = top4<N>(y4, a.scale, 4 * q, right, BW, R::kBS, R::kBZ, lane);
+                    const f4 Bv = top4<N>(y4, a.scale, 4 * q + h2, right, BW, R::kBS, R::kBZ, lane);
+                    if (!gstep) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) LVL(h2 - 2 + 4 * q + e) = f_minsum(A[e], Bv[e]);
+                    } else {
+                        const int q0 = s0 + 4 * q;
+                        const uint32_t sw = BWL(R::kBS + (q0 >> 5)), zw = BWL(R::kBZ + (q0 >> 5));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) LVL(h2 - 2 + 4 * q + e) = beta_val(sw, zw, (q0 + e) & 31) * A[e] + Bv[e];
+                    }
+                }
+                d = n - 2;
+            } else if (i == 0) {  // left child of the root: f on the channel LLRs
                 constexpr int h = N / 2;
                 for (int q = 0; q < h / 4; ++q) {
                     const f4 u = y4[q], v = y4[q + h / 4];
@@ -596,7 +640,7 @@ __global__ __launch_bounds__(64) void scl_lds_kernel(const CodeParams p, const A
                     const float ms = __shfl(m, src, 64);
                     if (src != lane) {
                         // live LLR levels: D in 1..n-1 with leaf i in the left child of its level-D node
-                        for (int D = 1; D < n; ++D) {
+                        for (int D = 1; D < (R::kTopRec ? n - 1 : n); ++D) {
                             if ((i >> (D - 1)) & 1) continue;
                             const int b0 = (1 << D) - 2;
                             for (int e = 0; e < (1 << D); ++e) LV[(b0 + e) * kWave + lane] = LV[(b0 + e) * kWave + src];

@@ -336,7 +336,7 @@ def test_fused_mc_sweep_equals_generate_then_decode(N, K, B):
         code = PolarCode(int(np.log2(N)), K, F=np.setdiff1d(np.arange(N), info))
     else:
         code = reference_polar_code(N, K)
-    assert code.fused_mc_supported()
+    assert code.fused_mc_supported() == (N <= 128)  # N = 256: the driver generates y (faster), the ABI still fuses
     snrs = [-1.0, 1.5, 3.0, 25.0]
     seed, off, si0 = 13, 12345, 2
     y = torch.empty(len(snrs), B, N, device=DEV)
