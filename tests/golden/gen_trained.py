@@ -53,7 +53,7 @@ CASES = {
                                 n_dec=4096, n_logit=512, n_mc=1 << 20, n_sc=1 << 17, seed_dec=31, seed_mc=37),
     "trained_crisp_64_32": dict(N=64, K=32, F=64, layers=2, snr_train=1.0, batch=4096, lr=1e-3,
                                 curriculum=[(8, 500), (12, 500), (16, 600), (20, 600), (24, 800), (28, 1000),
-                                            (32, 6000)],
+                                            (32, 3000)],
                                 n_dec=4096, n_logit=256, n_mc=1 << 20, n_sc=1 << 16, seed_dec=41, seed_mc=43),
 }
 

@@ -45,12 +45,15 @@ def check(hat, bits, ref_hat, ref_bits, hard, what, bd):
     first disagreeing information bit (sc_decode: later ones follow from it through the partial sums) --
     every one for sc_decode_soft, whose decisions feed nothing -- must sit where the decision LLR is
     within 2 E of zero.  Values: on codewords whose decisions agree (all codewords for sc_decode_soft),
-    hard decoded_bits bit-exact, soft ones within 2 E per entry, same NaN positions."""
+    hard decoded_bits bit-exact, soft ones within 2 E per entry, same NaN positions; those codewords are at least
+    95 % of the batch (a coarse floor: the bound, not the floor, is the parity criterion)."""
     from oracle import oracle as O
     bad = O.unexplained_disagreements(hat, ref_hat, bd["info"], bd["leaf"], bd["eleaf"], bd["feedback"])
     assert not bad, (what, "decision flips the bound does not explain (row, k, L, E)", bad[:5])
     if ref_bits is not None:
         rows = (hat == ref_hat).all(axis=1) if bd["feedback"] else np.ones(hat.shape[0], bool)
+        # coarse sanity floor beside the bound: the codewords left out of the value check below stay few
+        assert rows.mean() >= 0.95, (what, "codewords with identical decisions", float(rows.mean()))
         # finiteness may differ only at leaves whose computation met an inf/NaN (the bound is then not
         # finite): there an ulp of difference decides whether exp overflows (crafted |LLR| >> 1 words)
         nb, nr = np.isnan(bits[rows]), np.isnan(ref_bits[rows])

@@ -166,9 +166,10 @@ LSE_CASES = [(16, 8), (32, 16), (64, 32), (128, 64)]
 def test_sc_decode_lse_golden(oracle, N, K):
     """Exact-LSE SC (PolarCode.sc_decode, polar.py:209-279) incl. crafted rows that drive
     log_sum_avoid_NaN's inf/NaN patches.  glibc vs torch's Sleef exp/log/tanh differ by <= 2 ulp:
-    hard decisions bit-exact; soft decoded_bits: every finite entry within 2 E (the oracle's forward
-    error bound, oracle.sc_decode_lse_bound; measured max |diff| / 2E = 0.125), same NaN pattern, >= 99.9 %
-    of bits and >= 99 % of codewords identical."""
+    hard decisions bit-exact; soft decisions: every disagreement explained by the forward error bound (a leaf
+    LLR within 2 E of zero, oracle.sc_decode_lse_bound), and as a coarse sanity floor >= 97 % of the fixture's
+    codewords with identical msg_hat (one codeword in 24-48 per SNR point may flip; measured >= 99.2 %); soft decoded_bits on those codewords: every finite entry within 2 E (measured
+    max |diff| / 2E = 0.125) with the same NaN pattern."""
     d = golden(f"lse_{N}_{K}.npz")
     for tag, hard in (("hard", True), ("soft", False)):
         hat = np.empty_like(d[f"msg_hat_{tag}"])
@@ -180,6 +181,7 @@ def test_sc_decode_lse_golden(oracle, N, K):
         if hard:
             assert np.array_equal(hat, g) and np.array_equal(bits, gb), (N, tag)
         else:
+            assert (hat == g).all(axis=1).mean() >= 0.97, (N, tag)  # rows excluded below stay few
             for s in np.unique(d["snr"]):
                 m = d["snr"] == s
                 _, E, lf, el = oracle.sc_decode_lse_bound(d["y"][m], float(s), d["info"], leaves=True)
