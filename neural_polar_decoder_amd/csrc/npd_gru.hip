@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "npd_common.hpp"
@@ -403,20 +404,39 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
 }
 
 
-// =============================================================================== bf16 MFMA paths
+// =============================================================================== split 16-bit MFMA paths
 // precision 1 = bf16x3 split (a*b ~ ah*bh + ah*bl + al*bh, ~2^-16 relative per product),
 // precision 2 = plain bf16 (fp32 accumulate).  v_mfma_f32_32x32x16_bf16: 16x the fp32 MFMA rate.
+// precision 3 = fp16x3 split ("SPLIT 4" below): the same three products on v_mfma_f32_32x32x16_f16, whose
+// 11-bit significands make hi + lo a 22-bit split (a*b to ~2^-21 relative: fp32-class, against bf16x3's
+// 2^-16).  fp16's exponent range is handled by exact power-of-2 scaling: weights (and the y projection's
+// weights) x 2^8 on the host, states and received words x 2^8 at the split, so every accumulator holds
+// 2^16 x its value (biases / one-hot constants pre-scaled by 2^16, and the gate nonlinearities take the
+// 2^-16 in their exp2 constants: all exact).  Then hi and lo stay normal fp16 for |w| >= 5e-4 and
+// |h| >= 5e-4 (smaller terms contribute below 2^-33 absolute).
 // Same orientation as the fp32 kernel: an h' accumulator tile converts register-for-register into
 // the B fragments of the next step (registers 8s..8s+7 -> k-step s, cdna_hip_programming.md sec. 3).
 // Bias / one-hot / previous-decision terms stay an exact fp32 k-step (v_mfma_f32_32x32x2_f32).
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
+
+// SPLIT: 1 = bf16, 3 = bf16 hi + lo, 4 = fp16 hi + lo (scaled)
+template <int SPLIT>
+struct SplitT {
+    static constexpr bool kLo = SPLIT >= 3;
+    static constexpr bool kF16 = SPLIT == 4;
+    using V = std::conditional_t<kF16, hf8, bf8>;
+    using E = std::conditional_t<kF16, _Float16, __bf16>;
+    static constexpr float kIn = kF16 ? 256.0f : 1.0f;           // B-operand scale (states, y)
+    static constexpr float kAcc = kF16 ? 1.0f / 65536.0f : 1.0f;  // accumulator -> value
+};
 
 template <int F, int L, int SPLIT>
 struct GeoB {
     static constexpr int TT = 3 * F / 32, HT = F / 32, KB = F / 16;
     static constexpr int NG = (L == 2) ? 3 : 1;
     static constexpr int IMG = NG * TT * KB * 64 * 4;  // floats: one 16-B bf16x8 fragment per lane per step
-    static constexpr int NS = SPLIT == 3 ? 2 : 1;      // hi (+ lo) images
+    static constexpr int NS = SPLIT >= 3 ? 2 : 1;      // hi (+ lo) images
     static constexpr int OFF_X = NS * IMG;
     static constexpr int OFF_IN = OFF_X + NG * TT * 64;
     static constexpr int OFF_WL = OFF_IN + HT * 64;
@@ -442,52 +462,65 @@ struct ArgsB {
 __device__ __forceinline__ f16v mfma16(const bf8& a, const bf8& b, const f16v& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f16v mfma16(const hf8& a, const hf8& b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 
+// the gate pre-activations arrive as ACC x their value (ACC a power of 2): folded into the exp2 constants
+template <int SPLIT>
 __device__ __forceinline__ void gru_update_fast(f16v& h, const f16v& ar, const f16v& az, const f16v& ain,
                                                 const f16v& ahn) {
+    constexpr float acc = SplitT<SPLIT>::kAcc;
+    constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const float r = fast_sigmoid(ar[i]);
-        const float z = fast_sigmoid(az[i]);
-        const float nn = fast_tanh(ain[i] + ahn[i] * r);
+        const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
+        const float z = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * az[i]));
+        const float x = ain[i] + ahn[i] * r;
+        const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c2 * x)), -1.0f);
         h[i] = (h[i] - nn) * z + nn;
     }
 }
 
-// split the state tiles into bf16 B fragments (hi and, for SPLIT 3, lo)
+// split the state tiles into 16-bit B fragments (hi and, for SPLIT 3 / 4, lo)
 template <int HT, int SPLIT>
-__device__ __forceinline__ void to_frags(const f16v (&h)[HT], bf8 (&hi)[2 * HT], bf8 (&lo)[2 * HT]) {
+__device__ __forceinline__ void to_frags(const f16v (&h)[HT], typename SplitT<SPLIT>::V (&hi)[2 * HT],
+                                         typename SplitT<SPLIT>::V (&lo)[2 * HT]) {
+    using S = SplitT<SPLIT>;
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float v = h[t][8 * s + j];
-                const __bf16 b = (__bf16)v;
+                const float v = h[t][8 * s + j] * S::kIn;
+                const typename S::E b = (typename S::E)v;
                 hi[2 * t + s][j] = b;
-                if (SPLIT == 3) lo[2 * t + s][j] = (__bf16)(v - (float)b);
+                if (S::kLo) lo[2 * t + s][j] = (typename S::E)(v - (float)b);
             }
 }
 
 template <int TT, int KB, int NT, int SPLIT, int IMG>
 __device__ __forceinline__ void gemm_bf(const f4* __restrict__ smem4, int g, int t0, int lane, f16v (&acc)[NT],
-                                        const bf8 (&hi)[KB], const bf8 (&lo)[KB]) {
+                                        const typename SplitT<SPLIT>::V (&hi)[KB],
+                                        const typename SplitT<SPLIT>::V (&lo)[KB]) {
+    using V = typename SplitT<SPLIT>::V;
 #pragma unroll
     for (int q = 0; q < KB; ++q) {
-        bf8 ah[NT], al[NT];
+        V ah[NT], al[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const f4 v = smem4[((g * TT + t0 + t) * KB + q) * 64 + lane];
-            ah[t] = __builtin_bit_cast(bf8, v);
-            if (SPLIT == 3) al[t] = __builtin_bit_cast(bf8, smem4[IMG / 4 + ((g * TT + t0 + t) * KB + q) * 64 + lane]);
+            ah[t] = __builtin_bit_cast(V, v);
+            if (SplitT<SPLIT>::kLo)
+                al[t] = __builtin_bit_cast(V, smem4[IMG / 4 + ((g * TT + t0 + t) * KB + q) * 64 + lane]);
         }
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             acc[t] = mfma16(ah[t], hi[q], acc[t]);
-            if (SPLIT == 3) {
+            if (SplitT<SPLIT>::kLo) {
                 acc[t] = mfma16(ah[t], lo[q], acc[t]);
                 acc[t] = mfma16(al[t], hi[q], acc[t]);
             }
@@ -498,6 +531,9 @@ __device__ __forceinline__ void gemm_bf(const f4* __restrict__ smem4, int g, int
 template <int F, int L, int SPLIT>
 __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(const ArgsB a) {
     using G = GeoB<F, L, SPLIT>;
+    using S = SplitT<SPLIT>;
+    using V = typename S::V;
+    using E = typename S::E;
     constexpr int TT = G::TT, HT = G::HT, KB = G::KB, IMG = G::IMG;
     extern __shared__ __attribute__((aligned(16))) f4 smem4[];
     const float* smem = reinterpret_cast<const float*>(smem4);
@@ -530,19 +566,19 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
             for (int q = 0; q < nq; ++q) {
                 const f4 y0 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half);
                 const f4 y1 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half + 4);
-                bf8 yh, yl;
+                V yh, yl;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float v = j < 4 ? y0[j] : y1[j - 4];
-                    yh[j] = (__bf16)v;
-                    if (SPLIT == 3) yl[j] = (__bf16)(v - (float)yh[j]);
+                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
+                    yh[j] = (E)v;
+                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
                 }
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
-                    const bf8 wh = __builtin_bit_cast(bf8, a.wy[(t * nq + q) * 64 + lane]);
+                    const V wh = __builtin_bit_cast(V, a.wy[(t * nq + q) * 64 + lane]);
                     P[t] = mfma16(wh, yh, P[t]);
-                    if (SPLIT == 3) {
-                        const bf8 wl = __builtin_bit_cast(bf8, a.wy[a.wy_lo + (t * nq + q) * 64 + lane]);
+                    if (S::kLo) {
+                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nq + q) * 64 + lane]);
                         P[t] = mfma16(wh, yl, P[t]);
                         P[t] = mfma16(wl, yh, P[t]);
                     }
@@ -560,7 +596,7 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
             const int jj = a.rev ? N - 1 - ii : ii;
             const float xbe = half ? xb : 1.0f;
             {
-                bf8 fh[KB], fl[KB];
+                V fh[KB], fl[KB];
                 to_frags<HT, SPLIT>(h0, fh, fl);
                 f16v acc[TT];
 #pragma unroll
@@ -573,11 +609,11 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
 #pragma unroll
                 for (int j = 0; j < HT; ++j) {
                     const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
-                    gru_update_fast(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                    gru_update_fast<SPLIT>(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
                 }
             }
             if constexpr (L == 2) {
-                bf8 fh[KB], fl[KB], gh[KB], gl[KB];
+                V fh[KB], fl[KB], gh[KB], gl[KB];
                 to_frags<HT, SPLIT>(h0, fh, fl);
                 to_frags<HT, SPLIT>(h1, gh, gl);
                 f16v acc1[TT];
@@ -597,7 +633,7 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
 #pragma unroll
                 for (int j = 0; j < HT; ++j) {
                     ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
-                    gru_update_fast(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
+                    gru_update_fast<SPLIT>(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             }
             float part = 0.0f;
@@ -634,6 +670,30 @@ static float bf16_to_f(uint16_t b) {
     memcpy(&f, &u, 4);
     return f;
 }
+// IEEE binary16, round to nearest even (finite inputs within the fp16 range; subnormals handled)
+static uint16_t f16_rne(float f) {
+    const _Float16 h = (_Float16)f;  // clang lowers the host conversion with round-to-nearest-even
+    uint16_t b;
+    memcpy(&b, &h, 2);
+    return b;
+}
+static float f16_to_f(uint16_t b) {
+    _Float16 h;
+    memcpy(&h, &b, 2);
+    return (float)h;
+}
+// 16-bit split of v: SPLIT 4 -> fp16 of v * 2^8; else bf16 of v
+template <int SPLIT>
+static void split16(float v, uint16_t& hi, uint16_t& lo) {
+    if (SPLIT == 4) {
+        const float s = v * 256.0f;
+        hi = f16_rne(s);
+        lo = f16_rne(s - f16_to_f(hi));
+    } else {
+        hi = bf16_rne(v);
+        lo = bf16_rne(v - bf16_to_f(hi));
+    }
+}
 
 // img: fp32 image of GeoB (bf16 fragments stored as raw bytes inside the float array)
 template <int F, int L, int SPLIT>
@@ -667,18 +727,21 @@ static void build_image_bf(const float* W, int N, int onehot, std::vector<float>
                         const int th = q >> 1, s = q & 1;
                         const int colk = 32 * th + 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
                         const float v = mats[g][(size_t)row * F + colk];
-                        const uint16_t hi = bf16_rne(v);
+                        uint16_t hi, lo;
+                        split16<SPLIT>(v, hi, lo);
                         const size_t e = ((((size_t)(g * TT + t) * KB + q) * 64 + l) * 8 + j);
                         u16[e] = hi;
-                        if (SPLIT == 3) u16[(size_t)GB::IMG * 2 + e] = bf16_rne(v - bf16_to_f(hi));
+                        if (SPLIT >= 3) u16[(size_t)GB::IMG * 2 + e] = lo;
                     }
-    for (int i = 0; i < GB::NG * TT * 64; ++i) img[GB::OFF_X + i] = img32[G32::OFF_X + i];
-    for (int i = 0; i < HT * 64; ++i) img[GB::OFF_IN + i] = img32[G32::OFF_IN + i];
+    // the [1, x] k-step constants enter the accumulators directly: x 2^16 for the scaled fp16 split
+    const float kc = SPLIT == 4 ? 65536.0f : 1.0f;
+    for (int i = 0; i < GB::NG * TT * 64; ++i) img[GB::OFF_X + i] = img32[G32::OFF_X + i] * kc;
+    for (int i = 0; i < HT * 64; ++i) img[GB::OFF_IN + i] = img32[G32::OFF_IN + i] * kc;
     for (int i = 0; i < 2 * HT * 16; ++i) img[GB::OFF_WL + i] = img32[G32::OFF_WL + i];
     // y projection fragments: k-step q pairs lanes' y[16q + 8h + j]
     const int nq = N / 16;
     const size_t per = (size_t)TT * nq * 64 * 8;  // bf16 elements per image
-    wy.assign((per * (SPLIT == 3 ? 2 : 1) + 1) / 2, 0.0f);
+    wy.assign((per * (SPLIT >= 3 ? 2 : 1) + 1) / 2, 0.0f);
     uint16_t* w16 = reinterpret_cast<uint16_t*>(wy.data());
     for (int t = 0; t < TT; ++t)
         for (int q = 0; q < nq; ++q)
@@ -688,9 +751,10 @@ static void build_image_bf(const float* W, int N, int onehot, std::vector<float>
                     const int k = 16 * q + 8 * (l >> 5) + j;
                     const float v = wih[0][(size_t)row * Din + k];
                     const size_t e = (((size_t)t * nq + q) * 64 + l) * 8 + j;
-                    const uint16_t hi = bf16_rne(v);
+                    uint16_t hi, lo;
+                    split16<SPLIT>(v, hi, lo);
                     w16[e] = hi;
-                    if (SPLIT == 3) w16[per + e] = bf16_rne(v - bf16_to_f(hi));
+                    if (SPLIT >= 3) w16[per + e] = lo;
                 }
     wy_lo = (int64_t)(per / 8);  // in 16-B fragments
 }
@@ -943,7 +1007,8 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     NPD_ARG(F <= 64 || gru::wide_lds_bytes(N, F, layers) <= 160 * 1024,
             "npd_gru_create: F = 512 with 2 layers needs N <= 128 (LDS holds both states and the tile's y)");
     NPD_ARG(layers == 1 || layers == 2, "npd_gru_create: 1 or 2 GRU layers supported");
-    NPD_ARG(precision >= 0 && precision <= 2, "npd_gru_create: precision must be 0 (fp32), 1 (bf16x3) or 2 (bf16)");
+    NPD_ARG(precision >= 0 && precision <= 3,
+            "npd_gru_create: precision must be 0 (fp32), 1 (bf16x3), 2 (bf16) or 3 (fp16x3, scaled)");
     NPD_ARG(precision == 0 || N % 16 == 0, "npd_gru_create: bf16 paths need N % 16 == 0");
     const int Din = N + (onehot ? 2 : 1);
     int64_t expect = (int64_t)3 * F * Din + (int64_t)3 * F * F + 6 * F;
@@ -957,6 +1022,7 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     do {                                                                                               \
         if (precision == 0) gru::build_image<FF, LL>(weights, N, onehot, img, wy, b_lin);              \
         else if (precision == 1) gru::build_image_bf<FF, LL, 3>(weights, N, onehot, img, wy, b_lin, wy_lo); \
+        else if (precision == 3) gru::build_image_bf<FF, LL, 4>(weights, N, onehot, img, wy, b_lin, wy_lo); \
         else gru::build_image_bf<FF, LL, 1>(weights, N, onehot, img, wy, b_lin, wy_lo);               \
     } while (0)
     if (F == 512 && layers == 2) gru::build_image<512, 2>(weights, N, onehot, img, wy, b_lin);
@@ -1029,8 +1095,10 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
         b.y = y; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
         b.rev = a.rev; b.onehot = a.onehot; b.b_lin = g->b_lin; b.wy_lo = g->wy_lo;
         for (int w = 0; w < kMaxWords; ++w) b.info[w] = a.info[w];
-#define NPD_LBF(FF, LL) \
-        return g->precision == 1 ? gru::launch_bf<FF, LL, 3>(g, b, s) : gru::launch_bf<FF, LL, 1>(g, b, s)
+#define NPD_LBF(FF, LL)                                                                                   \
+        return g->precision == 1   ? gru::launch_bf<FF, LL, 3>(g, b, s)                                     \
+               : g->precision == 3 ? gru::launch_bf<FF, LL, 4>(g, b, s)                                     \
+                                   : gru::launch_bf<FF, LL, 1>(g, b, s)
         if (g->F == 64 && g->layers == 2) NPD_LBF(64, 2);
         if (g->F == 64) NPD_LBF(64, 1);
         if (g->layers == 2) NPD_LBF(32, 2);

@@ -98,9 +98,11 @@ class RNN_decoder:
     'y_input' runs fused on the GPU.
 
     ``precision`` (keyword, not in the reference): "fp32" (default; the reference's arithmetic),
-    "bf16x3" (split-bf16 MFMA, ~fp32 accuracy) or "bf16" (plain bf16 MFMA, fp32 accumulation)."""
+    "fp16x3" (scaled hi + lo fp16 split on the fp16 MFMA: three products per multiply, fp32 accumulation;
+    held to the fp32 path's tolerance, tests/test_gru_gpu.py), "bf16x3" (split-bf16, ~2^-16 relative per
+    product) or "bf16" (plain bf16 MFMA, fp32 accumulation).  The split paths cover hidden sizes <= 64."""
 
-    PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16": 2}
+    PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16": 2, "fp16x3": 3}
 
     def __init__(self, decoding_type, N, info_inds, onehot=False, reverse_order=False, precision="fp32"):
         if precision not in self.PRECISIONS:

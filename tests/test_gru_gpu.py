@@ -74,6 +74,43 @@ def test_gru_genie_frozen_values():
     assert np.all(np.abs(out[:, d["info"]]) <= 1.0)
 
 
+@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev"])
+def test_gru_decode_fp16x3_meets_fp32_tolerance(name):
+    """The scaled fp16x3 split path (precision "fp16x3": hi + lo fp16 parts of weights x 2^8 and states x 2^8,
+    three v_mfma_f32_32x32x16_f16 products per multiply, fp32 accumulation) held to the FP32 path's bars on
+    the reference's golden words: logits within 2e-5, >= 99.9 % of information bits and >= 99 % of
+    codewords identical.  (The F <= 64 fixtures: the split kernels cover hidden sizes up to 64.)"""
+    d = golden(f"{name}.npz")
+    net, dec = build(d, "fp16x3")
+    y = torch.from_numpy(d["y"]).to(DEV)
+    out, logits = dec.decode(net, False, y, return_logits=True)
+    out, logits = out.cpu().numpy(), logits.cpu().numpy()
+    info = d["info"]
+    assert (out[:, info] == d["decoded"][:, info]).mean() >= 0.999
+    same = (out == d["decoded"]).all(1)
+    assert same.mean() >= 0.99, same.mean()
+    assert np.abs(logits[same] - d["logits"][same]).max() < LOGIT_ATOL
+    frozen = np.setdiff1d(np.arange(int(d["N"])), info)
+    assert np.all(out[:, frozen] == 1.0)
+
+
+def test_gru_fp16x3_vs_oracle_ragged():
+    """fp16x3 against the C oracle on a ragged Monte-Carlo batch (fp32 bars)."""
+    from oracle import oracle as O
+    d = golden("gru_polar_64_32.npz")
+    net, dec = build(d, "fp16x3")
+    from neural_polar_decoder_amd import reference_polar_code
+    code = reference_polar_code(64, 32)
+    _, _, y = code.mc_generate(3000 + 7, 1.0, seed=11, device=DEV, want_msg=False)
+    out, logits = dec.decode(net, False, y, return_logits=True)
+    sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    od, ol = O.gru_decode(y.cpu().numpy(), sd, 64, 64, 2, d["info"], onehot=True, want_logits=True)
+    out, logits = out.cpu().numpy(), logits.cpu().numpy()
+    same = (out == od).all(1)
+    assert same.mean() >= 0.99
+    assert np.abs(logits[same] - ol[same]).max() < LOGIT_ATOL
+
+
 # bf16 MFMA variants (not the reference's arithmetic; opt-in). Tolerances:
 #   bf16x3 (hi/lo split, ~2^-16 relative per product, fast exp2/rcp gates): logits within 2e-3 absolute
 #          on agreeing codewords, >= 99.5 % information-bit agreement, >= 97 % codeword agreement.

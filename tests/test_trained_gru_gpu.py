@@ -26,18 +26,20 @@ LOGIT_ATOL = 2e-5
 CASES = ["trained_crisp_32_16", "trained_crisp_64_32"]
 
 
-def build(d):
+def build(d, precision="fp32"):
     from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
     N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
     net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).to(DEV).eval()
     net.load_state_dict({k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w.")})
-    return net, RNN_decoder("y_input", N, d["info"], onehot=True)
+    return net, RNN_decoder("y_input", N, d["info"], onehot=True, precision=precision)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
 @pytest.mark.parametrize("name", CASES)
-def test_trained_gru_decisions_match_reference(name):
+def test_trained_gru_decisions_match_reference(name, precision):
+    """fp32: the reference's arithmetic; fp16x3: the split fp16 path, held to the same bars."""
     d = trained_fixture(name)
-    net, dec = build(d)
+    net, dec = build(d, precision)
     info = d["info"]
     for si in range(len(d["snr"])):
         _, y = trained_words(d, si)
