@@ -321,12 +321,32 @@ def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
     t = timer(step, iters=2, warm=1)
     # the GRU kernel alone, HIP events on its stream (one launch = one SNR point's 2^20 words)
     ms = event_ms(lambda: dec.decode(net, False, yall[2]), 3, stream)
+    # the same step on the fp16x3 split path (held to the fp32 path's tolerance, tests/test_gru_gpu.py)
+    net16, dec16, _, _ = crisp_model(code, dev, precision="fp16x3")
+    c16 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+
+    def step16():
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)
+        for si in range(len(snrs)):
+            count_errors(msg, dec16.decode(net16, False, yall[si]), c16[si], cols=code.info_positions)
+
+    t16 = timer(step16, iters=2, warm=1)
+    ms16 = event_ms(lambda: dec16.decode(net16, False, yall[2]), 3, stream)
+    allreduce(c16, _sum(), world)
     allreduce(c_gru, _sum(), world)
     n = 3 * world * B
     cg = c_gru.cpu().numpy()
+    c16n = c16.cpu().numpy()
     flop_cw = gru_flop_per_cw(N_CODE, 64)
     tf = flop_cw * B / (ms / 1e3) / 1e12
+    fp16x3 = {"value": world * len(snrs) * B / t16, "ms_per_step": t16 * 1e3, "gru_avg_launch_ms": ms16,
+              "gru_bit_errors_vs_fp32_path": [int(a) - int(b) for a, b in zip(c16n[:, 0], cg[:, 0])],
+              "gru_block_errors_vs_fp32_path": [int(a) - int(b) for a, b in zip(c16n[:, 1], cg[:, 1])],
+              "note": "GRU on the scaled hi+lo fp16 split (3 v_mfma_f32_32x32x16_f16 products per multiply, fp32 "
+                      "accumulation), held to the fp32 path's tolerance; not the reference's arithmetic, so the "
+                      "record's value stays the fp32 path"}
     return {"value": world * len(snrs) * B / t, "unit": "codewords/s (each decoded by SC and by the GRU)",
+            "fp16x3_path": fp16x3,
             "ms_per_step": t * 1e3, "weights": wdesc,
             "roofline": {"bound": "mfma", "kernel": "gru_decode_kernel<64,2,4> (fp32 v_mfma_f32_32x32x2_f32)",
                          "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "frac": tf / FP32_PEAK_TF,
@@ -491,9 +511,13 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
         n = world * B  # counted once per SNR (the timer's single call); the event pass does not count
         flop_cw = gru_flop_per_cw(128, 64)
         tf = flop_cw * B / (ms / 1e3) / 1e12
+        net16, dec16 = seeded_crisp(code, 64, 2, seed=0, device=dev, precision="fp16x3")
+        dec16.decode(net16, False, ys[0][:64])
+        ms16 = event_ms(lambda: dec16.decode(net16, False, ys[2]), 1, stream)
         out["pac_gru"] = {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
                           "avg_launch_ms": ms, "algorithmic_flop_per_cw": flop_cw, "achieved_tflops": tf,
                           "peak_tflops_fp32": FP32_PEAK_TF, "frac": tf / FP32_PEAK_TF,
+                          "fp16x3_avg_launch_ms": ms16,
                           "total_codewords": world * len(snrs) * B,
                           "ber": {str(s): float(cc[i, 0]) / (n * 64) for i, s in enumerate(snrs)},
                           "bler": {str(s): float(cc[i, 1]) / n for i, s in enumerate(snrs)},

@@ -592,12 +592,13 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
             h1[t] = zero;
         }
         float xb = 1.0f;
+        // B fragments of h0: split once per update, used by layer 1 of this step and layer 0 of the next
+        V fh[KB], fl[KB];
+        to_frags<HT, SPLIT>(h0, fh, fl);
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             const float xbe = half ? xb : 1.0f;
             {
-                V fh[KB], fl[KB];
-                to_frags<HT, SPLIT>(h0, fh, fl);
                 f16v acc[TT];
 #pragma unroll
                 for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
@@ -612,8 +613,9 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
                     gru_update_fast<SPLIT>(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
                 }
             }
+            if constexpr (L == 1) to_frags<HT, SPLIT>(h0, fh, fl);
             if constexpr (L == 2) {
-                V fh[KB], fl[KB], gh[KB], gl[KB];
+                V gh[KB], gl[KB];
                 to_frags<HT, SPLIT>(h0, fh, fl);
                 to_frags<HT, SPLIT>(h1, gh, gl);
                 f16v acc1[TT];
