@@ -547,7 +547,8 @@ def scl_leg(code64, dev, y64, snr, world, timer):
         lambda: c256.scl_decode_mc(y2, 1.0, 4, SEED, 0, cnt), 2, stream), "batch_per_gpu": B2}
     return {"value": res["N64_L4"]["value"], "unit": "codewords/s", "list_size": 4, "batch_per_gpu": B,
             "avg_launch_ms": res["N64_L4"]["avg_launch_ms"], "L8": res["N64_L8"], "polar_256_128_L4": res["N256_L4"],
-            "bound": "VALU/LDS (per-path SC + list bookkeeping; HBM traffic is not the limit)",
+            "bound": "latency (profiles/round3/pmc_secondary.json: N=256 L=4 LDS-array busy 0.12 of cycles, VALU issue "
+                     "0.085, waves waiting 0.55 of cycles at 1 wave/SIMD; N=64 L=4 LDS 0.35, VALU 0.23)",
             "config": "scl_decode(L) (polar.py:793-876), Polar(64,32) at 2 dB and Polar(256,128) at 1 dB, "
                       "decode + fused BER/BLER counts"}
 
@@ -564,7 +565,10 @@ def lse_leg(code, dev, y, snr, world, timer):
         res[tag] = {"value": world * B / t,
                     "avg_launch_ms": event_ms(lambda: code.sc_decode(yb, snr, hard_decision=hard), 2, stream)}
     return {"value": res["soft"]["value"], "unit": "codewords/s", "batch_per_gpu": B, "soft": res["soft"],
-            "hard": res["hard"], "bound": "transcendental VALU (exp/log per check node)",
+            "hard": res["hard"],
+            "bound": "VALU latency (profiles/round3/pmc_secondary.json: VALU issue 0.24-0.27 of peak, 2.0k "
+                     "transcendentals of ~15k VALU instructions per codeword, waves waiting 0.5 of cycles at 3 "
+                     "waves/SIMD: dependent exp -> log chains)",
             "config": "Polar(64,32) sc_decode exact-LSE (polar.py:209-279), 2 dB, msg_hat out"}
 
 
