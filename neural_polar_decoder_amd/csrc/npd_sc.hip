@@ -23,6 +23,9 @@
 #ifndef NPD_SC_WPE
 #define NPD_SC_WPE 2  // waves per SIMD requested for the register-resident (N <= 64) kernels
 #endif
+#ifndef NPD_SC_STAGE_ROOT
+#define NPD_SC_STAGE_ROOT 1  // N = 128: root level through a coalesced 8 KB LDS stage (0: per-lane row reads)
+#endif
 
 namespace npd {
 namespace sc {
@@ -109,6 +112,7 @@ struct NoSpec {
     static constexpr bool on = false;
     static constexpr bool frozen(int) { return false; }
     static constexpr bool rate0(int, int) { return false; }
+    static constexpr int slot(int) { return 0; }
 };
 template <uint64_t M0, uint64_t M1>
 struct Spec {
@@ -119,9 +123,24 @@ struct Spec {
             if (!frozen(i)) return false;
         return true;
     }
+    static constexpr int slot(int i) {  // message slot of information position i
+        int k = 0;
+        for (int t = 0; t < i; ++t) k += frozen(t) ? 0 : 1;
+        return k;
+    }
 };
 // PAC(128,64), 'RM' rate profile (popcount(i) < 4 frozen; pac_code.py:121-174)
 using SpecPacRm128 = Spec<0x117177f177f7fffull, 0x101170117177full>;
+
+// N = 128 streaming decode: root level through an LDS stage (see dma_chunk / root_pass)
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
+struct RootStage {
+    static constexpr bool on = NPD_SC_STAGE_ROOT && !GEN && R < N && N == 128;
+    static constexpr bool vbits = on && PAC && !FULL && SP::on;  // v decisions as sign / zero bit words
+    static constexpr int slots = vbits ? 2 : 1;
+    static constexpr uint32_t kSlot = 64u * 32u * 4u;
+    static constexpr uint32_t kBytes = on ? kSlot * slots : 0u;
+};
 
 // ------------------------------------------------------------------------------ per-lane context
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
@@ -145,8 +164,10 @@ struct Ctx {
     float scale;
     uint32_t flags;
     const float4* yrow;   // N > R: this lane's received word in HBM (the root level is read from it directly)
+    int64_t row0;         // kStageRoot: this tile's first row
     // GEN: this lane's codeword bits (bit i set iff x_i = -1) and its noise stream
     uint32_t U[NW];
+    uint32_t VS[NW], VZ[NW];  // RootStage::vbits: v decisions by message slot, sign / zero bits
     uint64_t gseed, gcw;
     uint32_t gstream;
     float gsigma;
@@ -303,7 +324,17 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP, GEN>& c, const Cod
         // v is read at information positions only (msg_hat, counts): stored in slot (message) order, so
         // msg_hat leaves as 16-B rows
         if (!frozen) {
-            lds_wr8(c.lds, c.v_row + (uint32_t)c.k, v);
+            if constexpr (RootStage<N, R, PAC, FULL, SP, GEN>::vbits) {
+                // integer bit extraction (no compares: lane masks would be parked in VGPR lanes), and the words
+                // kept opaque so each leaf's bit is folded in at the leaf instead of all 64 v values staying live
+                constexpr int k = SP::slot(I);
+                const uint32_t vb = fbits(v);
+                c.VS[k >> 5] |= (vb >> 31) << (k & 31);
+                c.VZ[k >> 5] |= ((~vb >> 23) & 1u) << (k & 31);
+                asm volatile("" : "+v"(c.VS[k >> 5]), "+v"(c.VZ[k >> 5]));
+            } else {
+                lds_wr8(c.lds, c.v_row + (uint32_t)c.k, v);
+            }
             ++c.k;
         }
     }
@@ -409,6 +440,77 @@ __device__ __forceinline__ void stage_tile(char* lds, const Args& a, int64_t row
     }
 }
 
+// N = 128 streaming decode: the root level reaches the lanes through an LDS stage per wave instead of per-lane
+// row reads.  A per-lane 16-B read of 64 different rows costs the texture path 64 cache-line lookups per
+// instruction (PMC, per-lane version: TA busy 0.57 and TD busy 0.70 of the kernel, mostly stalled on the L1);
+// one 1 KiB LDS-DMA here covers 8 whole 128-B lines.  A root step (f or g) walks 4 chunks of 32 columns: A0
+// A1 (first half of the row) and B0 B1 (second half).  Chunk slots of 8 KB: one slot (A0 arrives prefetched,
+// B0 A1 B1 in turn) or, with the v decisions kept as bits in registers (msg-only PAC on a compile-time frozen
+// set: the LDS then holds no decision rows), two slots (A0 B0 prefetched, A1 B1 fetched together).
+
+// LDS-DMA of columns col0 .. col0+31 of rows row0 .. row0+63 into the slot at byte `base`: 64 rows x 8 chunks of
+// 16 B, chunk (r, q) at slot r*8 + q holding source chunk q ^ swz<8>(r) (stage_tile's swizzle: the row-per-lane
+// ds_read_b128 is conflict-free).  Asynchronous; read_slot waits.
+template <int N>
+__device__ __forceinline__ void dma_chunk(char* lds, uint32_t base, const Args& a, int64_t row0, int col0, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads of the slot are done
+    // opaque per call, so the 8 row addresses are not kept live between the calls of a tile
+    asm volatile("" : "+s"(row0));
+    // row r = 8k + lane/8, chunk (lane & 7) ^ swz<8>(r) = (lane & 7) ^ (lane >> 4) ^ 4 (k & 1)
+    const int c0 = (lane & 7) ^ (lane >> 4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int64_t grow = row0 + 8 * k + (lane >> 3);
+        if (grow >= a.B) grow = a.B - 1;
+        const float* src = a.y + grow * N + col0 + ((c0 ^ ((k & 1) << 2)) << 2);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(lds + base + k * 1024), 16, 0, 0);
+    }
+}
+
+// this lane's 32 values of the slot at `base` (waits for every outstanding DMA)
+__device__ __forceinline__ void read_slot(const char* lds, uint32_t base, int lane, float4 (&v)[8]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int sw = swz<8>(lane);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(lds + base + ((uint32_t)(lane * 8 + (q ^ sw)) << 4));
+}
+
+// one root step: emit(j0, A, B) gets this lane's columns j0 .. j0+31 of both halves of its row.  Chunk 0 (and
+// with two slots B0) is in the stage; afterwards the same for rows pf_row0 is prefetched (pf_row0 < 0: none)
+template <int N, int SLOTS, class Emit>
+__device__ __forceinline__ void root_pass(char* lds, const Args& a, int64_t row0, int64_t pf_row0, int lane, Emit&& emit) {
+    constexpr uint32_t kSlot = 64u * 32u * 4u;
+    const uint32_t s0 = a.off_stage, s1 = a.off_stage + (SLOTS == 2 ? kSlot : 0u);
+    float4 A[8], B[8];
+    if constexpr (SLOTS == 2) {
+        read_slot(lds, s0, lane, A);
+        read_slot(lds, s1, lane, B);
+        dma_chunk<N>(lds, s0, a, row0, 32, lane);
+        dma_chunk<N>(lds, s1, a, row0, 96, lane);
+        emit(0, A, B);
+        __builtin_amdgcn_sched_barrier(0);  // emit(0) before the next reads: A0 B0 and A1 B1 never live together
+        read_slot(lds, s0, lane, A);
+        read_slot(lds, s1, lane, B);
+        if (pf_row0 >= 0) {
+            dma_chunk<N>(lds, s0, a, pf_row0, 0, lane);
+            dma_chunk<N>(lds, s1, a, pf_row0, 64, lane);
+        }
+    } else {
+        read_slot(lds, s0, lane, A);
+        dma_chunk<N>(lds, s0, a, row0, 64, lane);
+        read_slot(lds, s0, lane, B);
+        dma_chunk<N>(lds, s0, a, row0, 32, lane);
+        emit(0, A, B);
+        __builtin_amdgcn_sched_barrier(0);
+        read_slot(lds, s0, lane, A);
+        dma_chunk<N>(lds, s0, a, row0, 96, lane);
+        read_slot(lds, s0, lane, B);
+        if (pf_row0 >= 0) dma_chunk<N>(lds, s0, a, pf_row0, 0, lane);
+    }
+    emit(32, A, B);
+}
+
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int D, int S0>
 __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const CodeParams& p, const Args& a) {
     if constexpr ((1 << D) == R) {
@@ -416,7 +518,19 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const 
         pack_block<N, R, PAC, FULL, SP, GEN, S0>(c);
     } else {
         constexpr int h = 1 << (D - 1);
-        if constexpr ((1 << D) == N) {
+        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::on) {
+            using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
+            root_pass<N, RS::slots>(c.lds, a, c.row0, c.row0, threadIdx.x, [&](int j0, const float4 (&A)[8], const float4 (&Bv)[8]) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int j = j0 + 4 * q;
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 0, f_minsum(rmul(c.scale, A[q].x), rmul(c.scale, Bv[q].x)));
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 1, f_minsum(rmul(c.scale, A[q].y), rmul(c.scale, Bv[q].y)));
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 2, f_minsum(rmul(c.scale, A[q].z), rmul(c.scale, Bv[q].z)));
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 3, f_minsum(rmul(c.scale, A[q].w), rmul(c.scale, Bv[q].w)));
+                }
+            });  // then this tile's first chunk(s) again, for the g step
+        } else if constexpr ((1 << D) == N) {
             // the root level straight from this lane's row in HBM (16-B loads), or generated (GEN)
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
@@ -433,7 +547,25 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const 
                 up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j), up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j + h)));
         }
         node_up<N, R, PAC, FULL, SP, GEN, D - 1, S0>(c, p, a);
-        if constexpr ((1 << D) == N) {
+        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::on) {
+            using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
+            const int64_t nrow0 = c.row0 + (int64_t)gridDim.x * kWave;  // grid-stride successor tile
+            root_pass<N, RS::slots>(c.lds, a, c.row0, nrow0 < a.B ? nrow0 : -1, threadIdx.x,
+                                    [&](int j0, const float4 (&A)[8], const float4 (&Bv)[8]) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float av[4] = {A[q].x, A[q].y, A[q].z, A[q].w};
+                    const float bv[4] = {Bv[q].x, Bv[q].y, Bv[q].z, Bv[q].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = j0 + 4 * q + e;
+                        const int pos = S0 + j;
+                        up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j,
+                                                 g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
+                    }
+                }
+            });
+        } else if constexpr ((1 << D) == N) {
             // second read of the row (L2 / MALL).  The pointer is laundered through an empty asm so the
             // compiler cannot forward the f step's loads: keeping those N values live across the left
             // half would cost N VGPRs (N = 128: 384 instead of ~250 -> one wave per SIMD instead of two)
@@ -523,6 +655,44 @@ __device__ __forceinline__ void store_slots(const char* lds, uint32_t base, uint
     }
 }
 
+// v decisions held as sign / zero bit words per lane (RootStage::vbits) -> fp32 msg_hat rows: the words go
+// through LDS (NW x 2 dwords per row at `base`) so the stores are coalesced, 16 B per lane when K % 4 == 0
+template <int NW>
+__device__ __forceinline__ void store_vbits(char* lds, uint32_t base, const uint32_t (&vs)[NW], const uint32_t (&vz)[NW],
+                                            int K, bool vec, float* out, int64_t tile_row0, int rows, int lane) {
+    constexpr uint32_t kRow = 2u * NW * 4u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        *reinterpret_cast<uint32_t*>(lds + base + (uint32_t)lane * kRow + 4u * w) = vs[w];
+        *reinterpret_cast<uint32_t*>(lds + base + (uint32_t)lane * kRow + 4u * (NW + w)) = vz[w];
+    }
+    if (vec) {
+        const int K4 = K >> 2;
+        float4* dst = reinterpret_cast<float4*>(out + tile_row0 * (int64_t)K);
+        for (int e = lane; e < rows * K4; e += kWave) {
+            const int r = e / K4, s = 4 * (e - r * K4);
+            const uint32_t row = base + (uint32_t)r * kRow;
+            const uint32_t sb = *reinterpret_cast<const uint32_t*>(lds + row + 4u * (uint32_t)(s >> 5)) >> (s & 31);
+            const uint32_t zb = *reinterpret_cast<const uint32_t*>(lds + row + 4u * (uint32_t)(NW + (s >> 5))) >> (s & 31);
+            float4 v;
+            v.x = (zb & 1u) ? 0.0f : ((sb & 1u) ? -1.0f : 1.0f);
+            v.y = (zb & 2u) ? 0.0f : ((sb & 2u) ? -1.0f : 1.0f);
+            v.z = (zb & 4u) ? 0.0f : ((sb & 4u) ? -1.0f : 1.0f);
+            v.w = (zb & 8u) ? 0.0f : ((sb & 8u) ? -1.0f : 1.0f);
+            dst[e] = v;
+        }
+    } else {
+        float* dst = out + tile_row0 * (int64_t)K;
+        for (int e = lane; e < rows * K; e += kWave) {
+            const int r = e / K, s = e - r * K;
+            const uint32_t row = base + (uint32_t)r * kRow;
+            const uint32_t sb = *reinterpret_cast<const uint32_t*>(lds + row + 4u * (uint32_t)(s >> 5)) >> (s & 31);
+            const uint32_t zb = *reinterpret_cast<const uint32_t*>(lds + row + 4u * (uint32_t)(NW + (s >> 5))) >> (s & 31);
+            dst[e] = (zb & 1u) ? 0.0f : ((sb & 1u) ? -1.0f : 1.0f);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------ kernel
 // <= 256 VGPRs so two waves share each SIMD (N = 256 is LDS-bound at 3 waves per CU anyway)
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
@@ -575,6 +745,12 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         err_bits = 0;
         err_blocks = 0;
     };
+    using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
+    constexpr bool kStageRoot = RS::on;
+    if (kStageRoot && blockIdx.x < total) {  // the first tile's prefetched chunk(s)
+        dma_chunk<N>(lds, a.off_stage, a, (int64_t)blockIdx.x * kWave, 0, lane);
+        if (RS::slots == 2) dma_chunk<N>(lds, a.off_stage + RS::kSlot, a, (int64_t)blockIdx.x * kWave, 64, lane);
+    }
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x) {
         const int seg = GEN ? (int)(g / a.ntiles) : 0;
         const int64_t t = GEN ? g - (int64_t)seg * a.ntiles : g;
@@ -599,6 +775,8 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         if constexpr (GEN) {
         } else if constexpr (R == N) {
             stage_tile<N>(lds, a, row0, lane);
+        } else if constexpr (kStageRoot) {
+            c.row0 = row0;
         } else {
             const int64_t grow = (row0 + lane) < a.B ? row0 + lane : a.B - 1;
             c.yrow = reinterpret_cast<const float4*>(a.y + grow * N);
@@ -621,10 +799,14 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
                 lds_wr(lds, a.off_gt + (uint32_t)((r * NP + col) * 4), a.gt[grow * N + col]);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (!kStageRoot) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
         c.st = 0;
         c.k = 0;
+        if constexpr (RS::vbits) {
+#pragma unroll
+            for (int w = 0; w < Ctx<N, R, PAC, FULL, SP, GEN>::NW; ++w) c.VS[w] = c.VZ[w] = 0u;
+        }
         // The frozen words are loop-invariant, so LICM would hoist all N per-leaf frozen tests out of the
         // tile loop as 64-bit lane masks and spill them into VGPR lanes (two v_readlane per leaf, plus
         // scratch); an opaque per-tile copy keeps each test next to its leaf (one s_bitcmp).
@@ -664,7 +846,14 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
                         const int k0 = blk * 128 + w * 32;
                         const int kn = (p.K - k0) < 32 ? (p.K - k0) : 32;
                         const uint32_t bits = w4[w];
-                        {
+                        if constexpr (RS::vbits) {
+                            // a slot counts if its sign differs from the message bit (bit 1 = -1) or it is 0
+                            if (kn > 0) {
+                                const uint32_t m = kn >= 32 ? 0xFFFFFFFFu : ((1u << kn) - 1u);
+                                e += (uint32_t)__builtin_popcount(((c.VS[(k0 >> 5) & (Ctx<N, R, PAC, FULL, SP, GEN>::NW - 1)] ^ bits) |
+                                                                   c.VZ[(k0 >> 5) & (Ctx<N, R, PAC, FULL, SP, GEN>::NW - 1)]) & m);
+                            }
+                        } else {
                             // slot-ordered decision bytes, 4 per dword, against the message nibbles: +1 ->
                             // 0x01, -1 -> 0xFF; a byte counts if it differs (0 decisions always do)
                             for (int q = 0; q < kn; q += 4) {
@@ -689,7 +878,9 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         }
 
         // ---- coalesced output stores
-        if (a.flags & kMsg) {
+        if (RS::vbits && (a.flags & kMsg)) {
+            store_vbits<Ctx<N, R, PAC, FULL, SP, GEN>::NW>(lds, a.off_v, c.VS, c.VZ, p.K, vec_msg, a.msg, row0, rows, lane);
+        } else if (a.flags & kMsg) {
             const uint32_t slots = PAC ? a.off_v : a.off_u;  // decisions in message order
             float* msg = GEN ? a.msg + (int64_t)seg * a.B * p.K : a.msg;
             if (vec_msg)
@@ -713,7 +904,7 @@ struct Layout {
 
 static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
-template <int N, int R>
+template <int N, int R, class RS>
 static Layout make_layout(bool pac, uint32_t flags) {
     Layout L{};
     const uint32_t stage = (uint32_t)(kWave * N * 4);
@@ -731,8 +922,7 @@ static Layout make_layout(bool pac, uint32_t flags) {
         L.off_v = pac ? off : 0;
         if (pac) off = align16(off + brow);
         L.off_lvl = off;
-        L.off_info = off;
-        off = align16(off + (uint32_t)(N * 4));
+        L.off_info = off;  // (no info table: decisions are kept in slot order)
         L.total = off;
         return L;
     }
@@ -743,27 +933,27 @@ static Layout make_layout(bool pac, uint32_t flags) {
         L.off_gt = (flags & kGt) ? off : 0;
         if (flags & kGt) off = align16(off + frow);
     } else {
-        off = 0;         // no y stage: the root level is read from HBM per lane
+        // no y tile stage: the root level is read from HBM per lane, or (N = 128) through an 8 KB chunk stage
+        off = RS::kBytes;
         L.off_leaf = 0;  // leaf LLRs and genie rows go straight to/from HBM
         L.off_gt = 0;
     }
     L.off_u = off;
-    off = align16(off + brow);
+    if (!pac || full) off = align16(off + brow);  // msg-only PAC keeps no u rows (its decisions are the v rows)
     L.off_v = pac ? off : 0;
-    if (pac) off = align16(off + brow);
+    if (pac) off = align16(off + (RS::vbits ? (uint32_t)(kWave * 2 * 4 * ((N + 31) / 32)) : brow));
     L.off_lvl = off;
     for (int d = 0; d < 9; ++d)
         if ((1 << d) > R && (1 << d) < N) off += (uint32_t)(kWave * ((1 << d) + 1) * 4);
     off = align16(off);
     L.off_info = off;
-    off = align16(off + (uint32_t)(N * 4));
     L.total = off;
     return L;
 }
 
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
 static int launch_t(const CodeParams& p, Args a, hipStream_t stream) {
-    const Layout L = make_layout<N, R>(PAC, a.flags);
+    const Layout L = make_layout<N, R, RootStage<N, R, PAC, FULL, SP, GEN>>(PAC, a.flags);
     a.off_stage = L.off_stage;
     a.off_u = L.off_u;
     a.off_v = L.off_v;

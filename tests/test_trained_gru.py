@@ -28,5 +28,8 @@ def test_oracle_gru_trained_fixture(oracle, name):
         assert same.mean() >= 0.99
         m = min(n, d[f"logits_{si}"].shape[0])
         assert np.abs(lg[:m][same[:m]] - d[f"logits_{si}"][:m][same[:m]]).max() < LOGIT_ATOL
-        # the net is trained: its confident logits are far from the untrained fixtures' near-zero values
-        assert np.median(np.abs(d[f"logits_{si}"][:, info])) > 0.1
+        # the net is trained: its decisions beat a coin flip clearly (untrained nets sit at BER 0.5) and its
+        # information-position logits are away from zero (median |logit| 0.29-0.31 at N = 32, 0.08-0.09 at
+        # N = 64, whose shorter curriculum leaves it at BER 0.33-0.36)
+        assert (ref != msg[:n]).mean() < 0.42
+        assert np.median(np.abs(d[f"logits_{si}"][:, info])) > 0.05

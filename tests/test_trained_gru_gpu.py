@@ -96,9 +96,12 @@ def test_trained_gru_ber_curve_matches_reference(name):
         z_ber = (be / n - rbe / nr) / np.sqrt(v / n + vr / nr)
         assert abs(z_bler) < 4 and abs(z_ber) < 4, (s, p, pr, z_bler, be / (n * K), rbe / (nr * K), z_ber)
         bler.append(p)
-    offs = db_offsets(snrs, bler, snrs, [int(x) / nr for x in d["mc_blk_err"]], min_bler=1e-3)
-    for s, o in zip(snrs, offs):
-        if o is not None:
+    ref_bler = [int(x) / nr for x in d["mc_blk_err"]]
+    offs = db_offsets(snrs, bler, snrs, ref_bler, min_bler=1e-3)
+    for s, o, pr in zip(snrs, offs, ref_bler):
+        # a dB offset is resolvable only where the curve falls: the N = 64 net's BLER stays above 0.99 on the
+        # whole grid (flat in SNR), so there the z-tests above are the bar
+        if o is not None and pr < 0.9:
             assert abs(o) <= 0.05, (s, o)
     # the trained decoder decodes: far below the coin-flip 0.5 of untrained weights at 2 dB
     assert ours[2][0] / (n * K) < 0.4
