@@ -23,6 +23,9 @@
 #ifndef NPD_SC_WPE
 #define NPD_SC_WPE 2  // waves per SIMD requested for the register-resident (N <= 64) kernels
 #endif
+#ifndef NPD_SC_ROOT_REGS
+#define NPD_SC_ROOT_REGS 0  // experiment: msg-only PAC(128) keeps its whole root row in VGPRs (1 wave per SIMD)
+#endif
 #ifndef NPD_SC_STAGE_ROOT
 #define NPD_SC_STAGE_ROOT 1  // N = 128: root level through a coalesced 8 KB LDS stage (0: per-lane row reads)
 #endif
@@ -73,9 +76,23 @@ __device__ __forceinline__ float rmul(float a, float b) {
     return r;
 }
 
+// sign(a) sign(b) min(|a|, |b|) in two VALU ops: med3(|a|, -|a|, b) = clamp(b, -|a|, |a|) has the magnitude
+// min(|a|, |b|) and the sign of b; xor in the sign of a (v_med3_f32 + v_bitop3_b32).  Equal in value to the
+// reference's product form (a zero may differ only in its sign bit, which no later step reads).
 __device__ __forceinline__ float f_minsum(float a, float b) {
-    const float m = __builtin_fminf(__builtin_fabsf(a), __builtin_fabsf(b));
-    return bitsf(fbits(m) | ((fbits(a) ^ fbits(b)) & 0x80000000u));
+    const float m = __builtin_amdgcn_fmed3f(__builtin_fabsf(a), -__builtin_fabsf(a), b);
+    return bitsf(__builtin_amdgcn_bitop3_b32(fbits(m), fbits(a), 0x80000000u, 0x78));  // m ^ (a & 0x80000000)
+}
+
+// fl32(s * v) for 4 values in two packed multiplies (each product rounded, never contracted: see rmul)
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 rmul4(float s, float4 v) {
+    f2v lo = {v.x, v.y}, hi = {v.z, v.w};
+    const f2v ss = {s, s};
+    lo = lo * ss;
+    hi = hi * ss;
+    asm("" : "+v"(lo), "+v"(hi));
+    return make_float4(lo.x, lo.y, hi.x, hi.y);
 }
 
 // sign(x) in {-1, 0, +1} (torch.sign): copy the sign bit onto 1.0, 0 for +-0
@@ -138,8 +155,11 @@ struct RootStage {
     static constexpr bool on = NPD_SC_STAGE_ROOT && !GEN && R < N && N == 128;
     static constexpr bool vbits = on && PAC && !FULL && SP::on;  // v decisions as sign / zero bit words
     static constexpr int slots = vbits ? 2 : 1;
+    static constexpr bool regs = NPD_SC_ROOT_REGS == 1 && vbits;  // whole tile staged, row held in registers
+    // regs2: A0 A1 B0 of the row held in registers, B1 resident in the second slot for the whole tile
+    static constexpr bool regs2 = NPD_SC_ROOT_REGS == 2 && vbits;
     static constexpr uint32_t kSlot = 64u * 32u * 4u;
-    static constexpr uint32_t kBytes = on ? kSlot * slots : 0u;
+    static constexpr uint32_t kBytes = regs ? 64u * N * 4u : (on ? kSlot * slots : 0u);
 };
 
 // ------------------------------------------------------------------------------ per-lane context
@@ -168,6 +188,7 @@ struct Ctx {
     // GEN: this lane's codeword bits (bit i set iff x_i = -1) and its noise stream
     uint32_t U[NW];
     uint32_t VS[NW], VZ[NW];  // RootStage::vbits: v decisions by message slot, sign / zero bits
+    float4 yr[(N + 3) / 4];   // RootStage::regs: this lane's received word
     uint64_t gseed, gcw;
     uint32_t gstream;
     float gsigma;
@@ -301,6 +322,33 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP, GEN>& c, const Cod
         const float lf = L + (frozen ? p.infty : 0.0f);
         write_leaf<N, R, PAC, FULL, SP, GEN, I>(c, lf);
         u = use_gt ? genie<N, R, PAC, FULL, SP, GEN, I>(c) : sgn_bits(lf);
+    } else if constexpr (!FULL) {
+        // msg-only PAC leaf on integer bits: conv(+1) = (-1)^parity(st & taps) (pac_code.py:188-193); a frozen
+        // leaf decides it (pac_code.py:545-551); an information leaf decides u = sign(L) and v = +1 when u equals
+        // conv(+1), -1 when it is the opposite, 0 when L = 0 (state unchanged) (pac_code.py:553-568) -- so v's
+        // sign is sign(L) xor the parity, and no float compares are needed
+        const uint32_t cnt = (uint32_t)__builtin_popcount(c.st & p.tapmask);
+        if (frozen) {
+            u = bitsf(0x3f800000u | (cnt << 31));
+            c.st = (c.st << 1) & p.smask;
+        } else {
+            const uint32_t Lb = fbits(L);
+            const bool nz = (Lb << 1) != 0u;
+            const uint32_t negb = ((Lb >> 31) ^ cnt) & 1u;
+            u = nz ? bitsf((Lb & 0x80000000u) | 0x3f800000u) : 0.0f;
+            const uint32_t sh = ((c.st << 1) | negb) & p.smask;
+            c.st = nz ? sh : c.st;
+            if constexpr (RootStage<N, R, PAC, FULL, SP, GEN>::vbits) {
+                // bits folded in at the leaf (opaque words: the 64 decisions do not stay live to the tile end)
+                constexpr int k = SP::slot(I);
+                c.VS[k >> 5] |= negb << (k & 31);
+                c.VZ[k >> 5] |= (nz ? 0u : 1u) << (k & 31);
+                asm volatile("" : "+v"(c.VS[k >> 5]), "+v"(c.VZ[k >> 5]));
+            } else {
+                lds_wr8(c.lds, c.v_row + (uint32_t)c.k, nz ? (negb ? -1.0f : 1.0f) : 0.0f);
+            }
+            ++c.k;
+        }
     } else {
         write_leaf<N, R, PAC, FULL, SP, GEN, I>(c, L);
         const float u0 = (__builtin_popcount(c.st & p.tapmask) & 1) ? -1.0f : 1.0f;  // conv(+1) (pac_code.py:188-193)
@@ -320,21 +368,10 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP, GEN>& c, const Cod
             const uint32_t sh = ((c.st << 1) | (neg ? 1u : 0u)) & p.smask;
             c.st = (eq || neg) ? sh : c.st;
         }
-        // v is read at information positions only (msg_hat, counts)
         // v is read at information positions only (msg_hat, counts): stored in slot (message) order, so
         // msg_hat leaves as 16-B rows
         if (!frozen) {
-            if constexpr (RootStage<N, R, PAC, FULL, SP, GEN>::vbits) {
-                // integer bit extraction (no compares: lane masks would be parked in VGPR lanes), and the words
-                // kept opaque so each leaf's bit is folded in at the leaf instead of all 64 v values staying live
-                constexpr int k = SP::slot(I);
-                const uint32_t vb = fbits(v);
-                c.VS[k >> 5] |= (vb >> 31) << (k & 31);
-                c.VZ[k >> 5] |= ((~vb >> 23) & 1u) << (k & 31);
-                asm volatile("" : "+v"(c.VS[k >> 5]), "+v"(c.VZ[k >> 5]));
-            } else {
-                lds_wr8(c.lds, c.v_row + (uint32_t)c.k, v);
-            }
+            lds_wr8(c.lds, c.v_row + (uint32_t)c.k, v);
             ++c.k;
         }
     }
@@ -456,21 +493,24 @@ __device__ __forceinline__ void dma_chunk(char* lds, uint32_t base, const Args& 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads of the slot are done
     // opaque per call, so the 8 row addresses are not kept live between the calls of a tile
     asm volatile("" : "+s"(row0));
+    // a buffer descriptor over the tile's rows (wave-uniform): 32-bit offsets, and rows past B read as zeros
+    // (tail lanes decode them; their results are neither counted nor stored)
+    const int64_t nrows = (a.B - row0) < kWave ? (a.B - row0) : kWave;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + row0 * N), 0, (int)(nrows * N * 4), 0x00020000);
     // row r = 8k + lane/8, chunk (lane & 7) ^ swz<8>(r) = (lane & 7) ^ (lane >> 4) ^ 4 (k & 1)
     const int c0 = (lane & 7) ^ (lane >> 4);
+    const uint32_t v0 = (uint32_t)(((lane >> 3) * N + col0 + (c0 << 2)) * 4);
+    const uint32_t v1 = (uint32_t)(((lane >> 3) * N + col0 + ((c0 ^ 4) << 2)) * 4);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        int64_t grow = row0 + 8 * k + (lane >> 3);
-        if (grow >= a.B) grow = a.B - 1;
-        const float* src = a.y + grow * N + col0 + ((c0 ^ ((k & 1) << 2)) << 2);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(lds + base + k * 1024), 16, 0, 0);
-    }
+    for (int k = 0; k < 8; ++k)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + base + k * 1024), 16,
+                                                 (k & 1) ? v1 : v0, 8 * k * N * 4, 0, 0);
 }
 
-// this lane's 32 values of the slot at `base` (waits for every outstanding DMA)
+// this lane's 32 values of the slot at `base` (waits for every outstanding DMA unless WAIT is false)
+template <bool WAIT = true>
 __device__ __forceinline__ void read_slot(const char* lds, uint32_t base, int lane, float4 (&v)[8]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int sw = swz<8>(lane);
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(lds + base + ((uint32_t)(lane * 8 + (q ^ sw)) << 4));
@@ -511,23 +551,98 @@ __device__ __forceinline__ void root_pass(char* lds, const Args& a, int64_t row0
     emit(32, A, B);
 }
 
+// regs2: chunk col0 (32 columns) of the tile's rows into registers with coalesced 16-B buffer loads (load k:
+// rows 8k .. 8k+7, whole 128-B lines; lane: row 8k + lane/8, columns col0 + 4 (lane & 7)), and such a chunk into
+// a slot in dma_chunk's layout
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <int N>
+__device__ __forceinline__ void load_chunk_buf(const Args& a, int64_t row0, int col0, int lane, float4 (&v)[8]) {
+    const int64_t nrows = (a.B - row0) < kWave ? (a.B - row0) : kWave;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + row0 * N), 0, (int)(nrows * N * 4), 0x00020000);
+    const int vo = ((lane >> 3) * N + col0 + 4 * (lane & 7)) * 4;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, 8 * k * N * 4, 0));
+}
+
+__device__ __forceinline__ void put_slot(char* lds, uint32_t base, int lane, const float4 (&v)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int r = 8 * k + (lane >> 3);
+        *reinterpret_cast<float4*>(lds + base + ((uint32_t)(r * 8 + ((lane & 7) ^ swz<8>(r))) << 4)) = v[k];
+    }
+}
+
+// g at the root for position pos of the left half.  N = 2R: the left half is one register block whose combined
+// partial sums are still in c.beta (nothing has overwritten them yet), so g = u a + b as in the register levels
+// (u in {-1, 0, 1}: the product is exact, one rounding); otherwise from the packed sign / zero bits.
+template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
+__device__ __forceinline__ float root_g(const Ctx<N, R, PAC, FULL, SP, GEN>& c, int pos, float a, float b) {
+    if constexpr (N == 2 * R) return c.beta[pos] * a + b;
+    else return g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, a, b);
+}
+
+// RootStage::regs: the whole 64 x N tile by LDS-DMA through a buffer descriptor (32-bit offsets; rows past B
+// read as zeros), in stage_tile's swizzled layout (chunk (r, q) at slot r*C + q holds source chunk q ^ swz<C>(r))
+template <int N>
+__device__ __forceinline__ void stage_tile_buf(char* lds, const Args& a, int64_t row0, int lane) {
+    constexpr int C = N / 4;
+    static_assert(C == 32, "N = 128");
+    asm volatile("" : "+s"(row0));
+    const int64_t nrows = (a.B - row0) < kWave ? (a.B - row0) : kWave;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + row0 * N), 0, (int)(nrows * N * 4), 0x00020000);
+    // instruction k: rows 2k + lane/32, chunk (lane & 31) ^ swz<32>(r), swz<32>(r) = r & 15 = 2 (k & 7) + lane/32
+    const int hi = lane >> 5;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t vo = (uint32_t)((hi * N + 4 * ((lane & 31) ^ (2 * (k & 7) + hi))) * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + a.off_stage + k * 1024), 16,
+                                                 vo, 2 * k * N * 4, 0, 0);
+    }
+}
+
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN, int D, int S0>
 __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const CodeParams& p, const Args& a) {
     if constexpr ((1 << D) == R) {
         node_reg<N, R, PAC, FULL, SP, GEN, D, S0>(c, p, a);
-        pack_block<N, R, PAC, FULL, SP, GEN, S0>(c);
+        // the packed bits feed g steps above the register levels other than the root's (N = 2R: root_g reads
+        // c.beta, and no level lies between)
+        if constexpr (N > 2 * R) pack_block<N, R, PAC, FULL, SP, GEN, S0>(c);
     } else {
         constexpr int h = 1 << (D - 1);
-        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::on) {
+        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs2) {
+            float4 B1[8];
+            read_slot<false>(c.lds, a.off_stage + RootStage<N, R, PAC, FULL, SP, GEN>::kSlot, threadIdx.x, B1);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float4 A = rmul4(c.scale, c.yr[q]), Bv = rmul4(c.scale, q < 8 ? c.yr[16 + q] : B1[q & 7]);
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 0, f_minsum(A.x, Bv.x));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 1, f_minsum(A.y, Bv.y));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 2, f_minsum(A.z, Bv.z));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 3, f_minsum(A.w, Bv.w));
+            }
+            // the transit slot is free: the next tile's A0
+            const int64_t nrow0 = c.row0 + (int64_t)gridDim.x * kWave;
+            if (nrow0 < a.B) dma_chunk<N>(c.lds, a.off_stage, a, nrow0, 0, threadIdx.x);
+        } else if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs) {
+#pragma unroll
+            for (int q = 0; q < h / 4; ++q) {
+                const float4 A = rmul4(c.scale, c.yr[q]), Bv = rmul4(c.scale, c.yr[q + h / 4]);
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 0, f_minsum(A.x, Bv.x));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 1, f_minsum(A.y, Bv.y));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 2, f_minsum(A.z, Bv.z));
+                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 3, f_minsum(A.w, Bv.w));
+            }
+        } else if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::on) {
             using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
             root_pass<N, RS::slots>(c.lds, a, c.row0, c.row0, threadIdx.x, [&](int j0, const float4 (&A)[8], const float4 (&Bv)[8]) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int j = j0 + 4 * q;
-                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 0, f_minsum(rmul(c.scale, A[q].x), rmul(c.scale, Bv[q].x)));
-                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 1, f_minsum(rmul(c.scale, A[q].y), rmul(c.scale, Bv[q].y)));
-                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 2, f_minsum(rmul(c.scale, A[q].z), rmul(c.scale, Bv[q].z)));
-                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 3, f_minsum(rmul(c.scale, A[q].w), rmul(c.scale, Bv[q].w)));
+                    const float4 As = rmul4(c.scale, A[q]), Bs = rmul4(c.scale, Bv[q]);
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 0, f_minsum(As.x, Bs.x));
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 1, f_minsum(As.y, Bs.y));
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 2, f_minsum(As.z, Bs.z));
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j + 3, f_minsum(As.w, Bs.w));
                 }
             });  // then this tile's first chunk(s) again, for the g step
         } else if constexpr ((1 << D) == N) {
@@ -547,21 +662,51 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const 
                 up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j), up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j + h)));
         }
         node_up<N, R, PAC, FULL, SP, GEN, D - 1, S0>(c, p, a);
-        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::on) {
+        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs2) {
+            using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
+            float4 B1[8];
+            read_slot<false>(c.lds, a.off_stage + RS::kSlot, threadIdx.x, B1);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float4 As = rmul4(c.scale, c.yr[q]), Bs = rmul4(c.scale, q < 8 ? c.yr[16 + q] : B1[q & 7]);
+                const float av[4] = {As.x, As.y, As.z, As.w};
+                const float bv[4] = {Bs.x, Bs.y, Bs.z, Bs.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = S0 + 4 * q + e;
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + e, root_g(c, pos, av[e], bv[e]));
+                }
+            }
+            // the resident slot is free: the next tile's B1
+            const int64_t nrow0 = c.row0 + (int64_t)gridDim.x * kWave;
+            if (nrow0 < a.B) dma_chunk<N>(c.lds, a.off_stage + RS::kSlot, a, nrow0, 96, threadIdx.x);
+        } else if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs) {
+#pragma unroll
+            for (int q = 0; q < h / 4; ++q) {
+                const float4 As = rmul4(c.scale, c.yr[q]), Bs = rmul4(c.scale, c.yr[q + h / 4]);
+                const float av[4] = {As.x, As.y, As.z, As.w};
+                const float bv[4] = {Bs.x, Bs.y, Bs.z, Bs.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = S0 + 4 * q + e;
+                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + e, root_g(c, pos, av[e], bv[e]));
+                }
+            }
+        } else if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::on) {
             using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
             const int64_t nrow0 = c.row0 + (int64_t)gridDim.x * kWave;  // grid-stride successor tile
             root_pass<N, RS::slots>(c.lds, a, c.row0, nrow0 < a.B ? nrow0 : -1, threadIdx.x,
                                     [&](int j0, const float4 (&A)[8], const float4 (&Bv)[8]) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const float av[4] = {A[q].x, A[q].y, A[q].z, A[q].w};
-                    const float bv[4] = {Bv[q].x, Bv[q].y, Bv[q].z, Bv[q].w};
+                    const float4 As = rmul4(c.scale, A[q]), Bs = rmul4(c.scale, Bv[q]);
+                    const float av[4] = {As.x, As.y, As.z, As.w};
+                    const float bv[4] = {Bs.x, Bs.y, Bs.z, Bs.w};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int j = j0 + 4 * q + e;
                         const int pos = S0 + j;
-                        up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j,
-                                                 g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
+                        up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j, root_g(c, pos, av[e], bv[e]));
                     }
                 }
             });
@@ -584,7 +729,7 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const 
                 for (int e = 0; e < 4; ++e) {
                     const int pos = S0 + 4 * q + e;
                     up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + e,
-                                             g_bits(c.S[pos >> 5], c.Z[pos >> 5], pos & 31, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
+                                             root_g(c, pos, rmul(c.scale, av[e]), rmul(c.scale, bv[e])));
                 }
             }
         } else {
@@ -747,9 +892,18 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
     };
     using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
     constexpr bool kStageRoot = RS::on;
-    if (kStageRoot && blockIdx.x < total) {  // the first tile's prefetched chunk(s)
-        dma_chunk<N>(lds, a.off_stage, a, (int64_t)blockIdx.x * kWave, 0, lane);
-        if (RS::slots == 2) dma_chunk<N>(lds, a.off_stage + RS::kSlot, a, (int64_t)blockIdx.x * kWave, 64, lane);
+    if constexpr (RS::regs) {  // the first tile (whole)
+        if (blockIdx.x < total) stage_tile_buf<N>(lds, a, (int64_t)blockIdx.x * kWave, lane);
+    } else if constexpr (RS::regs2) {  // the first tile's A0 (transit slot) and B1 (resident slot)
+        if (blockIdx.x < total) {
+            dma_chunk<N>(lds, a.off_stage, a, (int64_t)blockIdx.x * kWave, 0, lane);
+            dma_chunk<N>(lds, a.off_stage + RS::kSlot, a, (int64_t)blockIdx.x * kWave, 96, lane);
+        }
+    } else if constexpr (kStageRoot) {  // the first tile's prefetched chunk(s)
+        if (blockIdx.x < total) {
+            dma_chunk<N>(lds, a.off_stage, a, (int64_t)blockIdx.x * kWave, 0, lane);
+            if (RS::slots == 2) dma_chunk<N>(lds, a.off_stage + RS::kSlot, a, (int64_t)blockIdx.x * kWave, 64, lane);
+        }
     }
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x) {
         const int seg = GEN ? (int)(g / a.ntiles) : 0;
@@ -775,6 +929,31 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         if constexpr (GEN) {
         } else if constexpr (R == N) {
             stage_tile<N>(lds, a, row0, lane);
+        } else if constexpr (RS::regs2) {
+            // A0 (prefetched) -> registers; B0, A1 through the transit slot; B1 stays in the resident slot
+            // (B0 and A1 come in together by coalesced loads into registers, then turn through the transit slot)
+            c.row0 = row0;
+            float4 t[8], gB0[8], gA1[8];
+            read_slot(lds, a.off_stage, lane, t);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c.yr[q] = t[q];
+            load_chunk_buf<N>(a, row0, 64, lane, gB0);
+            load_chunk_buf<N>(a, row0, 32, lane, gA1);
+            put_slot(lds, a.off_stage, lane, gB0);
+            read_slot<false>(lds, a.off_stage, lane, t);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c.yr[16 + q] = t[q];
+            put_slot(lds, a.off_stage, lane, gA1);
+            read_slot<false>(lds, a.off_stage, lane, t);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c.yr[8 + q] = t[q];
+        } else if constexpr (RS::regs) {
+            // the staged tile -> this lane's row in registers, then the next tile's DMA into the stage
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < N / 4; ++q) c.yr[q] = stage_chunk<N>(lds, a.off_stage, c.stage_row, c.sw, q);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (row0 + (int64_t)gridDim.x * kWave < a.B) stage_tile_buf<N>(lds, a, row0 + (int64_t)gridDim.x * kWave, lane);
         } else if constexpr (kStageRoot) {
             c.row0 = row0;
         } else {
