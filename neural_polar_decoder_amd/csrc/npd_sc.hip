@@ -23,9 +23,6 @@
 #ifndef NPD_SC_WPE
 #define NPD_SC_WPE 2  // waves per SIMD requested for the register-resident (N <= 64) kernels
 #endif
-#ifndef NPD_SC_ROOT_REGS
-#define NPD_SC_ROOT_REGS 0  // experiment: msg-only PAC(128) keeps its whole root row in VGPRs (1 wave per SIMD)
-#endif
 #ifndef NPD_SC_STAGE_ROOT
 #define NPD_SC_STAGE_ROOT 1  // N = 128: root level through a coalesced 8 KB LDS stage (0: per-lane row reads)
 #endif
@@ -42,6 +39,7 @@ enum Flags : uint32_t {
 };
 
 constexpr int kMaxSeg = 16;  // SNR points of one fused Monte-Carlo sweep launch
+constexpr int kRootModeDefault = 1;  // Spec::root of the streaming PAC(128,64) RM decode (measured best)
 
 struct Args {
     const float* y;
@@ -127,13 +125,17 @@ struct Geo {
 // (pac_code.py:545-551), whatever the channel says, so the f/g steps feeding it are skipped.
 struct NoSpec {
     static constexpr bool on = false;
+    static constexpr int root = 0;
     static constexpr bool frozen(int) { return false; }
     static constexpr bool rate0(int, int) { return false; }
     static constexpr int slot(int) { return 0; }
 };
-template <uint64_t M0, uint64_t M1>
+// ROOT (msg-only N = 128 decode, see RootStage): 0 = root level through the LDS stage at each root step (the
+// g step re-reads y; 2 waves per SIMD), 1 = the whole row staged once and held in registers (1 wave per SIMD)
+template <uint64_t M0, uint64_t M1, int ROOT = 0>
 struct Spec {
     static constexpr bool on = true;
+    static constexpr int root = ROOT;
     static constexpr bool frozen(int i) { return (((i < 64) ? (M0 >> i) : (M1 >> (i - 64))) & 1ull) != 0; }
     static constexpr bool rate0(int s0, int len) {
         for (int i = s0; i < s0 + len; ++i)
@@ -148,16 +150,23 @@ struct Spec {
 };
 // PAC(128,64), 'RM' rate profile (popcount(i) < 4 frozen; pac_code.py:121-174)
 using SpecPacRm128 = Spec<0x117177f177f7fffull, 0x101170117177full>;
+template <int ROOT>
+using SpecPacRm128R = Spec<0x117177f177f7fffull, 0x101170117177full, ROOT>;
 
-// N = 128 streaming decode: root level through an LDS stage (see dma_chunk / root_pass)
+// N = 128 streaming decode: the root level reaches the lanes through LDS-DMA (coalesced 1 KiB instructions)
+// instead of per-lane row reads (64 cache-line lookups per instruction: PMC TA busy 0.57, TD busy 0.70).
+//   on:    32-column chunks through one or two 8 KB slots at each root step (dma_chunk / root_pass); the g step
+//          reads y again (L2 misses: 2x the y bytes cross the fabric), 2 waves per SIMD
+//   regs:  (Spec::root == 1, msg-only PAC on a compile-time frozen set) the whole 32 KB tile is staged once and
+//          the row held in 128 VGPRs across the left subtree (1 wave per SIMD, LDS 34 KB per wave), the next
+//          tile's DMA landing meanwhile: y crosses once (PMC: 805.7 MB per 2^20 words = algorithmic)
+//   vbits: the v decisions kept as sign / zero bit words in registers instead of LDS rows
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
 struct RootStage {
     static constexpr bool on = NPD_SC_STAGE_ROOT && !GEN && R < N && N == 128;
     static constexpr bool vbits = on && PAC && !FULL && SP::on;  // v decisions as sign / zero bit words
     static constexpr int slots = vbits ? 2 : 1;
-    static constexpr bool regs = NPD_SC_ROOT_REGS == 1 && vbits;  // whole tile staged, row held in registers
-    // regs2: A0 A1 B0 of the row held in registers, B1 resident in the second slot for the whole tile
-    static constexpr bool regs2 = NPD_SC_ROOT_REGS == 2 && vbits;
+    static constexpr bool regs = SP::root == 1 && vbits;  // whole tile staged, row held in registers
     static constexpr uint32_t kSlot = 64u * 32u * 4u;
     static constexpr uint32_t kBytes = regs ? 64u * N * 4u : (on ? kSlot * slots : 0u);
 };
@@ -327,16 +336,17 @@ __device__ __forceinline__ void leaf(Ctx<N, R, PAC, FULL, SP, GEN>& c, const Cod
         // leaf decides it (pac_code.py:545-551); an information leaf decides u = sign(L) and v = +1 when u equals
         // conv(+1), -1 when it is the opposite, 0 when L = 0 (state unchanged) (pac_code.py:553-568) -- so v's
         // sign is sign(L) xor the parity, and no float compares are needed
+        // (the state word is not masked to the register length here: only its bits under the taps are read)
         const uint32_t cnt = (uint32_t)__builtin_popcount(c.st & p.tapmask);
         if (frozen) {
             u = bitsf(0x3f800000u | (cnt << 31));
-            c.st = (c.st << 1) & p.smask;
+            c.st = c.st << 1;
         } else {
             const uint32_t Lb = fbits(L);
             const bool nz = (Lb << 1) != 0u;
             const uint32_t negb = ((Lb >> 31) ^ cnt) & 1u;
             u = nz ? bitsf((Lb & 0x80000000u) | 0x3f800000u) : 0.0f;
-            const uint32_t sh = ((c.st << 1) | negb) & p.smask;
+            const uint32_t sh = (c.st << 1) | negb;
             c.st = nz ? sh : c.st;
             if constexpr (RootStage<N, R, PAC, FULL, SP, GEN>::vbits) {
                 // bits folded in at the leaf (opaque words: the 64 decisions do not stay live to the tile end)
@@ -507,10 +517,9 @@ __device__ __forceinline__ void dma_chunk(char* lds, uint32_t base, const Args& 
                                                  (k & 1) ? v1 : v0, 8 * k * N * 4, 0, 0);
 }
 
-// this lane's 32 values of the slot at `base` (waits for every outstanding DMA unless WAIT is false)
-template <bool WAIT = true>
+// this lane's 32 values of the slot at `base` (waits for every outstanding DMA)
 __device__ __forceinline__ void read_slot(const char* lds, uint32_t base, int lane, float4 (&v)[8]) {
-    if constexpr (WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int sw = swz<8>(lane);
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(lds + base + ((uint32_t)(lane * 8 + (q ^ sw)) << 4));
@@ -551,27 +560,6 @@ __device__ __forceinline__ void root_pass(char* lds, const Args& a, int64_t row0
     emit(32, A, B);
 }
 
-// regs2: chunk col0 (32 columns) of the tile's rows into registers with coalesced 16-B buffer loads (load k:
-// rows 8k .. 8k+7, whole 128-B lines; lane: row 8k + lane/8, columns col0 + 4 (lane & 7)), and such a chunk into
-// a slot in dma_chunk's layout
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-template <int N>
-__device__ __forceinline__ void load_chunk_buf(const Args& a, int64_t row0, int col0, int lane, float4 (&v)[8]) {
-    const int64_t nrows = (a.B - row0) < kWave ? (a.B - row0) : kWave;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + row0 * N), 0, (int)(nrows * N * 4), 0x00020000);
-    const int vo = ((lane >> 3) * N + col0 + 4 * (lane & 7)) * 4;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, 8 * k * N * 4, 0));
-}
-
-__device__ __forceinline__ void put_slot(char* lds, uint32_t base, int lane, const float4 (&v)[8]) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int r = 8 * k + (lane >> 3);
-        *reinterpret_cast<float4*>(lds + base + ((uint32_t)(r * 8 + ((lane & 7) ^ swz<8>(r))) << 4)) = v[k];
-    }
-}
-
 // g at the root for position pos of the left half.  N = 2R: the left half is one register block whose combined
 // partial sums are still in c.beta (nothing has overwritten them yet), so g = u a + b as in the register levels
 // (u in {-1, 0, 1}: the product is exact, one rounding); otherwise from the packed sign / zero bits.
@@ -609,24 +597,10 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const 
         if constexpr (N > 2 * R) pack_block<N, R, PAC, FULL, SP, GEN, S0>(c);
     } else {
         constexpr int h = 1 << (D - 1);
-        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs2) {
-            float4 B1[8];
-            read_slot<false>(c.lds, a.off_stage + RootStage<N, R, PAC, FULL, SP, GEN>::kSlot, threadIdx.x, B1);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float4 A = rmul4(c.scale, c.yr[q]), Bv = rmul4(c.scale, q < 8 ? c.yr[16 + q] : B1[q & 7]);
-                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 0, f_minsum(A.x, Bv.x));
-                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 1, f_minsum(A.y, Bv.y));
-                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 2, f_minsum(A.z, Bv.z));
-                up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 3, f_minsum(A.w, Bv.w));
-            }
-            // the transit slot is free: the next tile's A0
-            const int64_t nrow0 = c.row0 + (int64_t)gridDim.x * kWave;
-            if (nrow0 < a.B) dma_chunk<N>(c.lds, a.off_stage, a, nrow0, 0, threadIdx.x);
-        } else if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs) {
+        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs) {
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 A = rmul4(c.scale, c.yr[q]), Bv = rmul4(c.scale, c.yr[q + h / 4]);
+                const float4 A = c.yr[q], Bv = c.yr[q + h / 4];  // scaled at the tile start
                 up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 0, f_minsum(A.x, Bv.x));
                 up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 1, f_minsum(A.y, Bv.y));
                 up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + 2, f_minsum(A.z, Bv.z));
@@ -662,28 +636,10 @@ __device__ __forceinline__ void node_up(Ctx<N, R, PAC, FULL, SP, GEN>& c, const 
                 up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, j, f_minsum(up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j), up_get<N, R, PAC, FULL, SP, GEN, D>(c, a, j + h)));
         }
         node_up<N, R, PAC, FULL, SP, GEN, D - 1, S0>(c, p, a);
-        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs2) {
-            using RS = RootStage<N, R, PAC, FULL, SP, GEN>;
-            float4 B1[8];
-            read_slot<false>(c.lds, a.off_stage + RS::kSlot, threadIdx.x, B1);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float4 As = rmul4(c.scale, c.yr[q]), Bs = rmul4(c.scale, q < 8 ? c.yr[16 + q] : B1[q & 7]);
-                const float av[4] = {As.x, As.y, As.z, As.w};
-                const float bv[4] = {Bs.x, Bs.y, Bs.z, Bs.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int pos = S0 + 4 * q + e;
-                    up_put<N, R, PAC, FULL, SP, GEN, D - 1>(c, 4 * q + e, root_g(c, pos, av[e], bv[e]));
-                }
-            }
-            // the resident slot is free: the next tile's B1
-            const int64_t nrow0 = c.row0 + (int64_t)gridDim.x * kWave;
-            if (nrow0 < a.B) dma_chunk<N>(c.lds, a.off_stage + RS::kSlot, a, nrow0, 96, threadIdx.x);
-        } else if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs) {
+        if constexpr ((1 << D) == N && RootStage<N, R, PAC, FULL, SP, GEN>::regs) {
 #pragma unroll
             for (int q = 0; q < h / 4; ++q) {
-                const float4 As = rmul4(c.scale, c.yr[q]), Bs = rmul4(c.scale, c.yr[q + h / 4]);
+                const float4 As = c.yr[q], Bs = c.yr[q + h / 4];
                 const float av[4] = {As.x, As.y, As.z, As.w};
                 const float bv[4] = {Bs.x, Bs.y, Bs.z, Bs.w};
 #pragma unroll
@@ -788,8 +744,9 @@ __device__ __forceinline__ void store_slots(const char* lds, uint32_t base, uint
                                             int64_t tile_row0, int rows, int lane) {
     const int K4 = K >> 2;
     float4* dst = reinterpret_cast<float4*>(out + tile_row0 * (int64_t)K);
+    int r = lane / K4, c4 = lane - (lane / K4) * K4;  // stepped incrementally (no division per element)
+    const int dr = kWave / K4, dc = kWave - (kWave / K4) * K4;
     for (int e = lane; e < rows * K4; e += kWave) {
-        const int r = e / K4, c4 = e - r * K4;
         const uint32_t w = *reinterpret_cast<const uint32_t*>(lds + base + (uint32_t)r * stride_b + 4u * (uint32_t)c4);
         float4 v;
         v.x = (float)(int8_t)(w & 0xffu);
@@ -797,6 +754,12 @@ __device__ __forceinline__ void store_slots(const char* lds, uint32_t base, uint
         v.z = (float)(int8_t)((w >> 16) & 0xffu);
         v.w = (float)(int8_t)(w >> 24);
         dst[e] = v;
+        r += dr;
+        c4 += dc;
+        if (c4 >= K4) {
+            c4 -= K4;
+            ++r;
+        }
     }
 }
 
@@ -814,8 +777,11 @@ __device__ __forceinline__ void store_vbits(char* lds, uint32_t base, const uint
     if (vec) {
         const int K4 = K >> 2;
         float4* dst = reinterpret_cast<float4*>(out + tile_row0 * (int64_t)K);
+        // (row, column) of element e stepped incrementally: one division per tile, not per element
+        int r = lane / K4, c4 = lane - (lane / K4) * K4;
+        const int dr = kWave / K4, dc = kWave - (kWave / K4) * K4;
         for (int e = lane; e < rows * K4; e += kWave) {
-            const int r = e / K4, s = 4 * (e - r * K4);
+            const int s = 4 * c4;
             const uint32_t row = base + (uint32_t)r * kRow;
             const uint32_t sb = *reinterpret_cast<const uint32_t*>(lds + row + 4u * (uint32_t)(s >> 5)) >> (s & 31);
             const uint32_t zb = *reinterpret_cast<const uint32_t*>(lds + row + 4u * (uint32_t)(NW + (s >> 5))) >> (s & 31);
@@ -825,6 +791,12 @@ __device__ __forceinline__ void store_vbits(char* lds, uint32_t base, const uint
             v.z = (zb & 4u) ? 0.0f : ((sb & 4u) ? -1.0f : 1.0f);
             v.w = (zb & 8u) ? 0.0f : ((sb & 8u) ? -1.0f : 1.0f);
             dst[e] = v;
+            r += dr;
+            c4 += dc;
+            if (c4 >= K4) {
+                c4 -= K4;
+                ++r;
+            }
         }
     } else {
         float* dst = out + tile_row0 * (int64_t)K;
@@ -841,7 +813,7 @@ __device__ __forceinline__ void store_vbits(char* lds, uint32_t base, const uint
 // ------------------------------------------------------------------------------ kernel
 // <= 256 VGPRs so two waves share each SIMD (N = 256 is LDS-bound at 3 waves per CU anyway)
 template <int N, int R, bool PAC, bool FULL, class SP, bool GEN>
-__global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodeParams p, const Args a) {
+__global__ __launch_bounds__(64, SP::root == 1 ? 1 : NPD_SC_WPE) void sc_decode_kernel(const CodeParams p, const Args a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int n = log2c<N>();
     constexpr int C = Geo<N>::C;
@@ -894,11 +866,6 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
     constexpr bool kStageRoot = RS::on;
     if constexpr (RS::regs) {  // the first tile (whole)
         if (blockIdx.x < total) stage_tile_buf<N>(lds, a, (int64_t)blockIdx.x * kWave, lane);
-    } else if constexpr (RS::regs2) {  // the first tile's A0 (transit slot) and B1 (resident slot)
-        if (blockIdx.x < total) {
-            dma_chunk<N>(lds, a.off_stage, a, (int64_t)blockIdx.x * kWave, 0, lane);
-            dma_chunk<N>(lds, a.off_stage + RS::kSlot, a, (int64_t)blockIdx.x * kWave, 96, lane);
-        }
     } else if constexpr (kStageRoot) {  // the first tile's prefetched chunk(s)
         if (blockIdx.x < total) {
             dma_chunk<N>(lds, a.off_stage, a, (int64_t)blockIdx.x * kWave, 0, lane);
@@ -929,29 +896,14 @@ __global__ __launch_bounds__(64, NPD_SC_WPE) void sc_decode_kernel(const CodePar
         if constexpr (GEN) {
         } else if constexpr (R == N) {
             stage_tile<N>(lds, a, row0, lane);
-        } else if constexpr (RS::regs2) {
-            // A0 (prefetched) -> registers; B0, A1 through the transit slot; B1 stays in the resident slot
-            // (B0 and A1 come in together by coalesced loads into registers, then turn through the transit slot)
-            c.row0 = row0;
-            float4 t[8], gB0[8], gA1[8];
-            read_slot(lds, a.off_stage, lane, t);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) c.yr[q] = t[q];
-            load_chunk_buf<N>(a, row0, 64, lane, gB0);
-            load_chunk_buf<N>(a, row0, 32, lane, gA1);
-            put_slot(lds, a.off_stage, lane, gB0);
-            read_slot<false>(lds, a.off_stage, lane, t);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) c.yr[16 + q] = t[q];
-            put_slot(lds, a.off_stage, lane, gA1);
-            read_slot<false>(lds, a.off_stage, lane, t);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) c.yr[8 + q] = t[q];
         } else if constexpr (RS::regs) {
             // the staged tile -> this lane's row in registers, then the next tile's DMA into the stage
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int q = 0; q < N / 4; ++q) c.yr[q] = stage_chunk<N>(lds, a.off_stage, c.stage_row, c.sw, q);
+            // scaled once: the f and g steps both read fl32(scale * y)
+#pragma unroll
+            for (int q = 0; q < N / 4; ++q) c.yr[q] = rmul4(c.scale, c.yr[q]);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (row0 + (int64_t)gridDim.x * kWave < a.B) stage_tile_buf<N>(lds, a, row0 + (int64_t)gridDim.x * kWave, lane);
         } else if constexpr (kStageRoot) {
@@ -1172,6 +1124,11 @@ static int dispatch(const CodeParams& p, const Args& a, hipStream_t s) {
     }
 }
 
+static int root_mode() {  // NPD_SC_ROOT=0/1: root-level mode of the msg-only PAC(128,64) RM kernel (A/B); per call
+    const char* e = getenv("NPD_SC_ROOT");
+    return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : kRootModeDefault;
+}
+
 static bool spec_off() {  // NPD_SC_NOSPEC=1: generic frozen set everywhere (testing / A-B); read per call
     const char* e = getenv("NPD_SC_NOSPEC");
     return e && e[0] == '1';
@@ -1190,7 +1147,10 @@ static int run(const npd_code* code, Args a, hipStream_t s) {
     if (a.B == 0) return NPD_OK;
     const bool full = (a.flags & (kLeaf | kGt | kUhat)) != 0;
     if (code->p.pac && !full && code->p.N == 128 && !spec_off() && is_frozen_set(code->p, 0x117177f177f7fffull, 0x101170117177full))
-        return launch_t<128, 64, true, false, SpecPacRm128, false>(code->p, a, s);
+        switch (root_mode()) {
+            case 1: return launch_t<128, 64, true, false, SpecPacRm128R<1>, false>(code->p, a, s);
+            default: return launch_t<128, 64, true, false, SpecPacRm128, false>(code->p, a, s);
+        }
     if (code->p.pac) return full ? dispatch<true, true>(code->p, a, s) : dispatch<true, false>(code->p, a, s);
     return full ? dispatch<false, true>(code->p, a, s) : dispatch<false, false>(code->p, a, s);
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B builds of libnpd.so with npd_sc.hip compiled under experiment macros (tools/bin/libnpd_<name>.so; loaded
-# through NPD_LIB).  Usage: bash tools/build_sc_variants.sh "rr:-DNPD_SC_ROOT_REGS=1 -DNPD_SC_WPE=1" ...
+# through NPD_LIB).  Usage: bash tools/build_sc_variants.sh "name:-DNPD_SC_WPE=3" ...
 set -e
 cd "$(dirname "$0")/.."
 make -j8 lib >/dev/null

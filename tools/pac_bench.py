@@ -9,7 +9,7 @@ sys.path.insert(0, ".")
 from neural_polar_decoder_amd import PAC, reference_polar_code  # noqa: E402
 
 
-def ev(fn, it=3):
+def ev(fn, it=20):
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -32,8 +32,8 @@ def main():
         hat = torch.empty(B, K, device=dev)
         _, _, y = code.mc_generate(B, 2.0, 1, 2, 0, device=dev, want_msg=False)
         t_dec = ev(lambda: code.sc_decode_mc(y, 2.0, 1, 0, c[2], msg_hat=hat))
-        t_gen = ev(lambda: code.mc_generate(B, 2.0, 1, 2, 0, device=dev, want_msg=False))
-        t_fused = ev(lambda: code.sc_mc_sweep_fused(B, snrs, 1, 0, c)) / len(snrs)
+        t_gen = ev(lambda: code.mc_generate(B, 2.0, 1, 2, 0, device=dev, want_msg=False), 5)
+        t_fused = ev(lambda: code.sc_mc_sweep_fused(B, snrs, 1, 0, c), 5) / len(snrs)
         print(f"{name}: decode {t_dec:.3f} ms + generate {t_gen:.3f} ms per 2^20 | fused sweep {t_fused:.3f} ms per "
               f"2^20 per SNR", flush=True)
 
