@@ -30,6 +30,9 @@ struct npd_gru {
     float* wy;    // y-projection A operands (device)
     int64_t img_floats;
     int64_t wy_lo;
+    float* img16;  // 16-codeword split kernel's image (F = 64, 2 layers, split precisions), or NULL
+    float* wy16;
+    int64_t wy16_lo;
 };
 
 namespace npd {
@@ -1014,6 +1017,309 @@ static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
     return launch_check("gru_decode_bf_kernel launch");
 }
 
+// =============================================================================== split paths, 16-codeword waves
+// F = 64, 2 layers (the metric's CRISP GRU), split precisions, N a multiple of 32.  The 32-codeword split kernels
+// above need ~500 registers (P, both states, the gate accumulators): one wave per SIMD, and a step is one serial
+// chain (layer-0 GEMM -> update -> split -> layer-1 GEMM -> update -> output -> decision) that leaves the MFMA pipe
+// idle while the wave does its VALU work.  Here a wave owns 16 codewords on v_mfma_f32_16x16x32_{f16,bf16} (the same
+// FLOP per cycle as 32x32x16), so every register array halves and TWO waves share each SIMD: a 16-bit MFMA holds its
+// SIMD's vector issue for only 8 of its 16 cycles (MI355X_MICROARCH.md), so one wave's gate updates, splits and
+// output issue in the other wave's MFMA gaps.
+// 16x16x32 maps: lane l = 16 g + c holds D[row 4g + i][codeword c] (i = 0..3), A[row c][k 8g + j], B[k 8g + j][col c].
+// Hidden units form 16-row tiles ht = 0..3; K block kb (32 units) is tiles 2kb, 2kb + 1, with MFMA k index 8g + j
+// <-> hidden unit 16 (2kb + (j >> 2)) + 4g + (j & 3): an updated state tile converts register for register into the
+// next GEMM's B fragment (no lane movement); the host permutes the weight images to match.
+// Constants: layer 0's biases and one-hot column 0 enter P once per codeword, the x_i column is one FMA per
+// accumulator element, layer 1's biases initialise its accumulators from LDS: no fp32 k-step MFMAs.
+// The arithmetic per element (split products, fp32 accumulation, gate nonlinearities) is the 32-codeword kernels'.
+struct Geo16 {
+    static constexpr int RT = 12, KB = 2, NG = 3;    // 16-row gate tiles, 32-unit K blocks, weight matrices
+    static constexpr int IMG4 = NG * RT * KB * 64;   // 16-B fragments per split image
+    static constexpr int OFF_C = 2 * IMG4 * 4;       // floats: constants after the hi and lo images
+    static constexpr int C0L0 = OFF_C, C1L0 = OFF_C + 192, BHN0 = OFF_C + 384, C0L1 = OFF_C + 448,
+                         BHN1 = OFF_C + 640, WLIN = OFF_C + 704, TOTAL = OFF_C + 768;
+};
+
+__device__ __forceinline__ f4 mfma16s(const hf8& a, const hf8& b, const f4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 mfma16s(const bf8& a, const bf8& b, const f4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int SPLIT>
+__device__ __forceinline__ void update4(f4& h, const f4& ar, const f4& az, const f4& ain, const f4& ahn) {
+    constexpr float acc = SplitT<SPLIT>::kAcc;
+    constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
+        const float z = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * az[i]));
+        const float x = ain[i] + ahn[i] * r;
+        const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c2 * x)), -1.0f);
+        h[i] = (h[i] - nn) * z + nn;
+    }
+}
+
+// B fragments of a state: fragment kb, element j = tile 2kb + (j >> 2), register j & 3 (hi and, split, lo)
+template <int SPLIT>
+__device__ __forceinline__ void split16s(const f4 (&h)[4], typename SplitT<SPLIT>::V (&hi)[2],
+                                         typename SplitT<SPLIT>::V (&lo)[2]) {
+    using S = SplitT<SPLIT>;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = h[2 * kb + (j >> 2)][j & 3] * S::kIn;
+            const typename S::E b = (typename S::E)v;
+            hi[kb][j] = b;
+            if (S::kLo) lo[kb][j] = (typename S::E)(v - (float)b);
+        }
+}
+
+// acc[u] += W_g[row tile t[u]] . state over both K blocks
+template <int SPLIT, int NU>
+__device__ __forceinline__ void gemm16s(const f4* __restrict__ smem4, int g, const int (&t)[NU], int lane,
+                                        f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
+                                        const typename SplitT<SPLIT>::V (&bl)[2]) {
+    using G = Geo16;
+    using V = typename SplitT<SPLIT>::V;
+#pragma unroll
+    for (int kb = 0; kb < G::KB; ++kb) {
+        V ah[NU], al[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int idx = ((g * G::RT + t[u]) * G::KB + kb) * 64 + lane;
+            ah[u] = __builtin_bit_cast(V, smem4[idx]);
+            if (SplitT<SPLIT>::kLo) al[u] = __builtin_bit_cast(V, smem4[G::IMG4 + idx]);
+        }
+        asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            acc[u] = mfma16s(ah[u], bh[kb], acc[u]);
+            if (SplitT<SPLIT>::kLo) {
+                acc[u] = mfma16s(ah[u], bl[kb], acc[u]);
+                acc[u] = mfma16s(al[u], bh[kb], acc[u]);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ f4 fma4(float x, const f4& c, const f4& p) {
+    return f4{fmaf(x, c[0], p[0]), fmaf(x, c[1], p[1]), fmaf(x, c[2], p[2]), fmaf(x, c[3], p[3])};
+}
+
+#define NPD_GRU16_WPB 8
+template <int SPLIT>
+__global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a) {
+    using G = Geo16;
+    using S = SplitT<SPLIT>;
+    using V = typename S::V;
+    using E = typename S::E;
+    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
+    const float* smem = reinterpret_cast<const float*>(smem4);
+    {
+        const f4* src = reinterpret_cast<const f4*>(a.img);
+        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int g4 = lane >> 4;
+    const int col = lane & 15;
+    const int N = a.N;
+    const int nkb = N / 32;
+    const int64_t ntiles = (a.B + 15) / 16;
+    // rows 4 g4 .. 4 g4 + 3 of 16-row tile t of a constant vector
+    auto c4 = [&](int off, int t) -> f4 { return *reinterpret_cast<const f4*>(smem + off + 16 * t + 4 * g4); };
+    const f4 zero = {0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU16_WPB + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * NPD_GRU16_WPB) {
+        const int64_t cw = tile * 16 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        // ---- P = consts + W_ih0[:, :N] . y ; K block kb covers y[32 kb + 8 g4 .. + 7]
+        f4 P[G::RT];
+#pragma unroll
+        for (int t = 0; t < G::RT; ++t) P[t] = c4(G::C0L0, t);
+        {
+            const float* yr = a.y + cwc * N;
+            for (int kb = 0; kb < nkb; ++kb) {
+                const f4 y0 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4);
+                const f4 y1 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4 + 4);
+                V yh, yl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
+                    yh[j] = (E)v;
+                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
+                }
+#pragma unroll
+                for (int t = 0; t < G::RT; ++t) {
+                    const V wh = __builtin_bit_cast(V, a.wy[(t * nkb + kb) * 64 + lane]);
+                    P[t] = mfma16s(wh, yh, P[t]);
+                    if (S::kLo) {
+                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nkb + kb) * 64 + lane]);
+                        P[t] = mfma16s(wh, yl, P[t]);
+                        P[t] = mfma16s(wl, yh, P[t]);
+                    }
+                }
+            }
+        }
+        f4 h0[4], h1[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            h0[t] = zero;
+            h1[t] = zero;
+        }
+        V fh[2], fl[2];
+        split16s<SPLIT>(h0, fh, fl);
+        float xb = 1.0f;  // x_i column of the one-hot input (or the previous decision's sign)
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            // ================= layer 0, hidden tile by hidden tile (r, z, hn rows of tile ht)
+#pragma unroll
+            for (int ht = 0; ht < 4; ++ht) {
+                const int T[3] = {ht, 4 + ht, 8 + ht};
+                f4 acc[3] = {fma4(xb, c4(G::C1L0, ht), P[ht]), fma4(xb, c4(G::C1L0, 4 + ht), P[4 + ht]),
+                             c4(G::BHN0, ht)};
+                gemm16s<SPLIT, 3>(smem4, 0, T, lane, acc, fh, fl);
+                const f4 ain = fma4(xb, c4(G::C1L0, 8 + ht), P[8 + ht]);
+                update4<SPLIT>(h0[ht], acc[0], acc[1], ain, acc[2]);
+            }
+            V gh[2], gl[2];
+            split16s<SPLIT>(h1, gh, gl);
+            split16s<SPLIT>(h0, fh, fl);  // h0' for layer 1 and the next step's layer 0
+            // ================= layer 1: r, z = c + W_ih1 h0' + W_hh1 h1 ; in = c + W_ih1_n h0' ; hn = c + W_hh1_n h1
+#pragma unroll
+            for (int ht = 0; ht < 4; ++ht) {
+                const int T[3] = {ht, 4 + ht, 8 + ht};
+                f4 ai[3] = {c4(G::C0L1, ht), c4(G::C0L1, 4 + ht), c4(G::C0L1, 8 + ht)};
+                gemm16s<SPLIT, 3>(smem4, 1, T, lane, ai, fh, fl);
+                f4 ah[3] = {ai[0], ai[1], c4(G::BHN1, ht)};
+                gemm16s<SPLIT, 3>(smem4, 2, T, lane, ah, gh, gl);
+                update4<SPLIT>(h1[ht], ah[0], ah[1], ai[2], ah[2]);
+            }
+            // ================= output: Linear(F, 1), reduced over the four lane groups
+            float part = 0.0f;
+#pragma unroll
+            for (int ht = 0; ht < 4; ++ht) {
+                const f4 wl = c4(G::WLIN, ht);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) part += wl[i] * h1[ht][i];
+            }
+            part += __shfl_xor(part, 16, 64);
+            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+            float d;
+            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+            if (g4 == 0 && valid) {
+                a.decoded[cw * N + jj] = d;
+                if (a.logits) a.logits[cw * N + ii] = out;
+            }
+            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+        }
+    }
+}
+
+// image of gru16_kernel: weight fragments (hi, lo) in the 16x16x32 A-operand order, constants x kc
+template <int SPLIT>
+static void build_image16(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
+                          int64_t& wy_lo) {
+    using G = Geo16;
+    constexpr int F = 64, L = 2;
+    const int Din = N + (onehot ? 2 : 1);
+    const float* p = W;
+    const float* wih[2];
+    const float* whh[2];
+    const float* bih[2];
+    const float* bhh[2];
+    for (int l = 0; l < L; ++l) {
+        const int din = l == 0 ? Din : F;
+        wih[l] = p; p += (size_t)3 * F * din;
+        whh[l] = p; p += (size_t)3 * F * F;
+        bih[l] = p; p += 3 * F;
+        bhh[l] = p; p += 3 * F;
+    }
+    const float* wlin = p;
+    img.assign(G::TOTAL, 0.0f);
+    const float* mats[3] = {whh[0], wih[1], whh[1]};
+    uint16_t* u16 = reinterpret_cast<uint16_t*>(img.data());
+    for (int g = 0; g < G::NG; ++g)
+        for (int t = 0; t < G::RT; ++t)
+            for (int kb = 0; kb < G::KB; ++kb)
+                for (int l = 0; l < 64; ++l)
+                    for (int j = 0; j < 8; ++j) {
+                        const int row = 16 * t + (l & 15);
+                        const int hid = 16 * (2 * kb + (j >> 2)) + 4 * (l >> 4) + (j & 3);
+                        uint16_t hi, lo;
+                        split16<SPLIT>(mats[g][(size_t)row * F + hid], hi, lo);
+                        const size_t e = ((((size_t)(g * G::RT + t) * G::KB + kb) * 64 + l) * 8 + j);
+                        u16[e] = hi;
+                        if (SPLIT >= 3) u16[(size_t)G::IMG4 * 8 + e] = lo;
+                    }
+    const float kc = SPLIT == 4 ? 65536.0f : 1.0f;
+    auto col = [&](int row, int k) { return wih[0][(size_t)row * Din + k]; };
+    for (int row = 0; row < 3 * F; ++row) {
+        const bool rz = row < 2 * F;
+        // x_i enters as c0 + x_i c1 (one-hot: columns N, N + 1 -> c0 = w_N, c1 = w_{N+1} - w_N; else c1 = w_N)
+        const float c0x = onehot ? col(row, N) : 0.0f;
+        const float c1x = onehot ? col(row, N + 1) - col(row, N) : col(row, N);
+        img[G::C0L0 + row] = kc * (rz ? bih[0][row] + bhh[0][row] + c0x : bih[0][row] + c0x);
+        img[G::C1L0 + row] = kc * c1x;
+        img[G::C0L1 + row] = kc * (rz ? bih[1][row] + bhh[1][row] : bih[1][row]);
+    }
+    for (int j = 0; j < F; ++j) {
+        img[G::BHN0 + j] = kc * bhh[0][2 * F + j];
+        img[G::BHN1 + j] = kc * bhh[1][2 * F + j];
+        img[G::WLIN + j] = wlin[j];
+    }
+    const int nkb = N / 32;
+    const size_t per = (size_t)G::RT * nkb * 64 * 8;  // 16-bit elements per y-projection image
+    wy.assign((per * (SPLIT >= 3 ? 2 : 1) + 1) / 2, 0.0f);
+    uint16_t* w16 = reinterpret_cast<uint16_t*>(wy.data());
+    for (int t = 0; t < G::RT; ++t)
+        for (int kb = 0; kb < nkb; ++kb)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                    const int row = 16 * t + (l & 15);
+                    const int k = 32 * kb + 8 * (l >> 4) + j;
+                    uint16_t hi, lo;
+                    split16<SPLIT>(col(row, k), hi, lo);
+                    const size_t e = (((size_t)t * nkb + kb) * 64 + l) * 8 + j;
+                    w16[e] = hi;
+                    if (SPLIT >= 3) w16[per + e] = lo;
+                }
+    wy_lo = (int64_t)(per / 8);
+}
+
+static bool gru16_enabled() {  // NPD_GRU16=0: the 32-codeword split kernels (A/B)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NPD_GRU16");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
+template <int SPLIT>
+static int launch16(const ArgsB& a, hipStream_t s) {
+    auto kern = gru16_kernel<SPLIT>;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    const int64_t tiles = (a.B + 15) / 16;
+    const int64_t wgs = (tiles + NPD_GRU16_WPB - 1) / NPD_GRU16_WPB;
+    const int grid = grid_for(wgs, 1, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU16_WPB), (size_t)Geo16::TOTAL * 4, s, a);
+    return launch_check("gru16_kernel launch");
+}
+
 // =============================================================================== wide hidden sizes
 // F = 128 / 256 / 512 (the CRISP curriculum trains F = 512, 2 layers: run_crisp.sh).  The weights
 // (3 x 3F x F fp32 = 9.4 MB at F = 512) no longer fit in LDS, so the per-step matvecs of a 32-codeword
@@ -1279,14 +1585,28 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     g->N = N; g->F = F; g->layers = layers; g->onehot = onehot; g->precision = precision; g->b_lin = b_lin;
     g->img_floats = (int64_t)img.size();
     g->wy_lo = wy_lo;
+    std::vector<float> img16, wy16;
+    if (precision != 0 && F == 64 && layers == 2 && N % 32 == 0) {
+        if (precision == 1) gru::build_image16<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        else if (precision == 3) gru::build_image16<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        else gru::build_image16<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
+    }
     hipError_t e = hipGetDevice(&g->device);
     if (e == hipSuccess) e = hipMalloc(&g->img, img.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&g->wy, wy.size() * 4);
     if (e == hipSuccess) e = hipMemcpy(g->img, img.data(), img.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(g->wy, wy.data(), wy.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !img16.empty()) {
+        e = hipMalloc(&g->img16, img16.size() * 4);
+        if (e == hipSuccess) e = hipMalloc(&g->wy16, wy16.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(g->img16, img16.data(), img16.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(g->wy16, wy16.data(), wy16.size() * 4, hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         if (g->img) (void)hipFree(g->img);
         if (g->wy) (void)hipFree(g->wy);
+        if (g->img16) (void)hipFree(g->img16);
+        if (g->wy16) (void)hipFree(g->wy16);
         delete g;
         return hip_fail(e, "npd_gru_create");
     }
@@ -1298,6 +1618,8 @@ extern "C" int npd_gru_destroy(npd_gru* g) {
     if (!g) return NPD_OK;
     if (g->img) (void)hipFree(g->img);
     if (g->wy) (void)hipFree(g->wy);
+    if (g->img16) (void)hipFree(g->img16);
+    if (g->wy16) (void)hipFree(g->wy16);
     delete g;
     return NPD_OK;
 }
@@ -1332,6 +1654,14 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
         b.y = y; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
         b.rev = a.rev; b.onehot = a.onehot; b.b_lin = g->b_lin; b.wy_lo = g->wy_lo;
         for (int w = 0; w < kMaxWords; ++w) b.info[w] = a.info[w];
+        if (g->img16 && gru::gru16_enabled()) {
+            b.img = g->img16;
+            b.wy = reinterpret_cast<const gru::f4*>(g->wy16);
+            b.wy_lo = g->wy16_lo;
+            return g->precision == 1   ? gru::launch16<3>(b, s)
+                   : g->precision == 3 ? gru::launch16<4>(b, s)
+                                       : gru::launch16<1>(b, s);
+        }
 #define NPD_LBF(FF, LL)                                                                                   \
         return g->precision == 1   ? gru::launch_bf<FF, LL, 3>(g, b, s)                                     \
                : g->precision == 3 ? gru::launch_bf<FF, LL, 4>(g, b, s)                                     \
