@@ -41,6 +41,19 @@ namespace gru {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
+template <int N>
+struct IC {
+    static constexpr int value = N;
+};
+// compile-time loop: f(IC<i>{}) for i in [B, E)
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    if constexpr (B < E) {
+        f(IC<B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 template <int F, int L>
 struct Geo {
     static constexpr int TT = 3 * F / 32;  // 32-row tiles of the 3F gate rows
@@ -1225,6 +1238,235 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a
     }
 }
 
+// ---- software-pipelined variant (NPD_GRU16=2 A/B).  A wave's own VALU instructions issue in the gaps of its 16-bit
+// MFMAs (8 of the 16 cycles of a 16x16x32 are busy for vector issue, MI355X_MICROARCH.md), while another wave's
+// do not (profiles/round3/coissue.txt: an fp16 MFMA wave and an FMA wave on one SIMD take the sum of their times).
+// So each hidden tile's GEMM carries the update of the PREVIOUS tile (cut into 12 chunks of ~5 instructions:
+// element i, stage 0 exp2s / 1 rcps + n-gate input + exp2 / 2 rcp + blend), spread over its MFMA triples between
+// sched_barrier fences; the h1 update of tile 3, the output, the decision and the h1 split ride on the NEXT step's
+// layer-0 tile-0 GEMM (which needs only h0', not x_i: the x_i column and P are added after it).
+template <int SPLIT>
+struct Upd4 {
+    f4 er, ez, en, z;
+    template <int C>
+    __device__ __forceinline__ void step(f4& h, const f4& ar, const f4& az, const f4& ain, const f4& ahn) {
+        constexpr float acc = SplitT<SPLIT>::kAcc;
+        constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+        constexpr int i = C / 3, st = C % 3;
+        if constexpr (st == 0) {
+            er[i] = __builtin_amdgcn_exp2f(c1 * ar[i]);
+            ez[i] = __builtin_amdgcn_exp2f(c1 * az[i]);
+        } else if constexpr (st == 1) {
+            const float r = __builtin_amdgcn_rcpf(1.0f + er[i]);
+            z[i] = __builtin_amdgcn_rcpf(1.0f + ez[i]);
+            en[i] = __builtin_amdgcn_exp2f(c2 * (ain[i] + ahn[i] * r));
+        } else {
+            const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + en[i]), -1.0f);
+            h[i] = (h[i] - nn) * z[i] + nn;
+        }
+    }
+};
+
+template <int SPLIT>
+__device__ __forceinline__ void split_kb(const f4 (&h)[4], int kb, typename SplitT<SPLIT>::V (&hi)[2],
+                                         typename SplitT<SPLIT>::V (&lo)[2]) {
+    using S = SplitT<SPLIT>;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = h[2 * kb + (j >> 2)][j & 3] * S::kIn;
+        const typename S::E b = (typename S::E)v;
+        hi[kb][j] = b;
+        if (S::kLo) lo[kb][j] = (typename S::E)(v - (float)b);
+    }
+}
+
+
+// acc[u] += W_g[row tile t[u]] . state (both K blocks); work(IC<c>) for chunks C0 .. C0 + NCH - 1 spread evenly
+// over the 2 NU MFMA triples, one sched_barrier-fenced region per triple
+template <int SPLIT, int NU, int C0, int NCH, typename Work>
+__device__ __forceinline__ void gemm16i(const f4* __restrict__ smem4, int g, const int (&t)[NU], int lane,
+                                        f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
+                                        const typename SplitT<SPLIT>::V (&bl)[2], Work&& work) {
+    using G = Geo16;
+    using V = typename SplitT<SPLIT>::V;
+    constexpr int NT = 2 * NU;
+    V ah[2][NU], al[2][NU];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int idx = ((g * G::RT + t[u]) * G::KB + kb) * 64 + lane;
+            ah[kb][u] = __builtin_bit_cast(V, smem4[idx]);
+            if (SplitT<SPLIT>::kLo) al[kb][u] = __builtin_bit_cast(V, smem4[G::IMG4 + idx]);
+        }
+    asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
+    static_for<0, NT>([&](auto trc) {
+        constexpr int tr = decltype(trc)::value;
+        constexpr int kb = tr / NU, u = tr % NU;
+        acc[u] = mfma16s(ah[kb][u], bh[kb], acc[u]);
+        if (SplitT<SPLIT>::kLo) {
+            acc[u] = mfma16s(ah[kb][u], bl[kb], acc[u]);
+            acc[u] = mfma16s(al[kb][u], bh[kb], acc[u]);
+        }
+        static_for<C0 + NCH * tr / NT, C0 + NCH * (tr + 1) / NT>([&](auto cc) { work(cc); });
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+template <int SPLIT>
+__global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB a) {
+    using G = Geo16;
+    using S = SplitT<SPLIT>;
+    using V = typename S::V;
+    using E = typename S::E;
+    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
+    const float* smem = reinterpret_cast<const float*>(smem4);
+    {
+        const f4* src = reinterpret_cast<const f4*>(a.img);
+        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int g4 = lane >> 4;
+    const int col = lane & 15;
+    const int N = a.N;
+    const int nkb = N / 32;
+    const int64_t ntiles = (a.B + 15) / 16;
+    auto c4 = [&](int off, int t) -> f4 { return *reinterpret_cast<const f4*>(smem + off + 16 * t + 4 * g4); };
+    const f4 zero = {0.f, 0.f, 0.f, 0.f};
+    constexpr int T0[3] = {0, 4, 8};
+    auto nowork = [](auto) {};
+
+    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU16_WPB + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * NPD_GRU16_WPB) {
+        const int64_t cw = tile * 16 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        f4 P[G::RT];
+#pragma unroll
+        for (int t = 0; t < G::RT; ++t) P[t] = c4(G::C0L0, t);
+        {
+            const float* yr = a.y + cwc * N;
+            for (int kb = 0; kb < nkb; ++kb) {
+                const f4 y0 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4);
+                const f4 y1 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4 + 4);
+                V yh, yl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
+                    yh[j] = (E)v;
+                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
+                }
+#pragma unroll
+                for (int t = 0; t < G::RT; ++t) {
+                    const V wh = __builtin_bit_cast(V, a.wy[(t * nkb + kb) * 64 + lane]);
+                    P[t] = mfma16s(wh, yh, P[t]);
+                    if (S::kLo) {
+                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nkb + kb) * 64 + lane]);
+                        P[t] = mfma16s(wh, yl, P[t]);
+                        P[t] = mfma16s(wl, yh, P[t]);
+                    }
+                }
+            }
+        }
+        f4 h0[4], h1[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            h0[t] = zero;
+            h1[t] = zero;
+        }
+        V fh[2], fl[2], gh[2], gl[2];
+        split16s<SPLIT>(h0, fh, fl);
+        split16s<SPLIT>(h1, gh, gl);
+        float xb = 1.0f;
+        // layer 0, hidden tile 0 of step 0: W_hh0 h0 part (the x_i column and P are added at the top of the step)
+        f4 a0[3] = {zero, zero, c4(G::BHN0, 0)};
+        gemm16i<SPLIT, 3, 0, 0>(smem4, 0, T0, lane, a0, fh, fl, nowork);
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            Upd4<SPLIT> u;
+            // ================= layer 0
+            f4 ap[3] = {a0[0] + fma4(xb, c4(G::C1L0, 0), P[0]), a0[1] + fma4(xb, c4(G::C1L0, 4), P[4]), a0[2]};
+            f4 ainp = fma4(xb, c4(G::C1L0, 8), P[8]);
+            static_for<1, 4>([&](auto htc) {
+                constexpr int ht = decltype(htc)::value;
+                const int T[3] = {ht, 4 + ht, 8 + ht};
+                f4 acc[3] = {fma4(xb, c4(G::C1L0, ht), P[ht]), fma4(xb, c4(G::C1L0, 4 + ht), P[4 + ht]),
+                             c4(G::BHN0, ht)};
+                gemm16i<SPLIT, 3, 0, 12>(smem4, 0, T, lane, acc, fh, fl, [&](auto cc) {
+                    u.template step<decltype(cc)::value>(h0[ht - 1], ap[0], ap[1], ainp, ap[2]);
+                });
+                ainp = fma4(xb, c4(G::C1L0, 8 + ht), P[8 + ht]);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) ap[k] = acc[k];
+            });
+            // ================= layer 1, hidden tile 0: W_hh1 h1 beside h0 tile 3's update and the h0' split
+            f4 b[3] = {c4(G::C0L1, 0), c4(G::C0L1, 4), c4(G::BHN1, 0)};
+            gemm16i<SPLIT, 3, 0, 14>(smem4, 2, T0, lane, b, gh, gl, [&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c < 12) u.template step<c>(h0[3], ap[0], ap[1], ainp, ap[2]);
+                else split_kb<SPLIT>(h0, c - 12, fh, fl);
+            });
+            f4 bi[3] = {b[0], b[1], c4(G::C0L1, 8)};
+            gemm16i<SPLIT, 3, 0, 0>(smem4, 1, T0, lane, bi, fh, fl, nowork);
+            f4 q[4] = {bi[0], bi[1], bi[2], b[2]};  // r, z, in, hn of the previous layer-1 tile
+            float part = 0.0f;
+            static_for<1, 4>([&](auto htc) {
+                constexpr int ht = decltype(htc)::value;
+                const int T[3] = {ht, 4 + ht, 8 + ht};
+                f4 bb[3] = {c4(G::C0L1, ht), c4(G::C0L1, 4 + ht), c4(G::BHN1, ht)};
+                auto work = [&](auto cc) {
+                    constexpr int c = decltype(cc)::value;
+                    if constexpr (c < 12) {
+                        u.template step<c>(h1[ht - 1], q[0], q[1], q[2], q[3]);
+                    } else {
+                        const f4 wl = c4(G::WLIN, ht - 1);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) part = fmaf(wl[i], h1[ht - 1][i], part);
+                    }
+                };
+                gemm16i<SPLIT, 3, 0, 7>(smem4, 2, T, lane, bb, gh, gl, work);
+                f4 bbi[3] = {bb[0], bb[1], c4(G::C0L1, 8 + ht)};
+                gemm16i<SPLIT, 3, 7, 6>(smem4, 1, T, lane, bbi, fh, fl, work);
+                q[0] = bbi[0];
+                q[1] = bbi[1];
+                q[2] = bbi[2];
+                q[3] = bb[2];
+            });
+            // ================= tail: next step's layer-0 tile-0 GEMM beside h1 tile 3's update, the output, the
+            // decision and the h1 split
+            a0[0] = zero;
+            a0[1] = zero;
+            a0[2] = c4(G::BHN0, 0);
+            gemm16i<SPLIT, 3, 0, 15>(smem4, 0, T0, lane, a0, fh, fl, [&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c < 12) {
+                    u.template step<c>(h1[3], q[0], q[1], q[2], q[3]);
+                } else if constexpr (c == 12) {
+                    const f4 wl = c4(G::WLIN, 3);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) part = fmaf(wl[i], h1[3][i], part);
+                    part += __shfl_xor(part, 16, 64);
+                    const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+                    const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+                    float d;
+                    if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+                    else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+                    if (g4 == 0 && valid) {
+                        a.decoded[cw * N + jj] = d;
+                        if (a.logits) a.logits[cw * N + ii] = out;
+                    }
+                    const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+                    xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+                } else {
+                    split_kb<SPLIT>(h1, c - 13, gh, gl);
+                }
+            });
+        }
+    }
+}
+
 // image of gru16_kernel: weight fragments (hi, lo) in the 16x16x32 A-operand order, constants x kc
 template <int SPLIT>
 static void build_image16(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
@@ -1296,18 +1538,19 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
     wy_lo = (int64_t)(per / 8);
 }
 
-static bool gru16_enabled() {  // NPD_GRU16=0: the 32-codeword split kernels (A/B)
+static int gru16_mode() {  // NPD_GRU16=0: the 32-codeword split kernels; 1: gru16_kernel; 2: gru16p_kernel (A/B)
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("NPD_GRU16");
-        v = (e && e[0] == '0') ? 0 : 1;
+        v = (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
     }
-    return v == 1;
+    return v;
 }
+static bool gru16_enabled() { return gru16_mode() != 0; }
 
 template <int SPLIT>
 static int launch16(const ArgsB& a, hipStream_t s) {
-    auto kern = gru16_kernel<SPLIT>;
+    auto kern = gru16_mode() == 2 ? gru16p_kernel<SPLIT> : gru16_kernel<SPLIT>;
     static bool attr = false;
     if (!attr) {
         NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
