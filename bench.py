@@ -400,10 +400,14 @@ def gru_leg(code, dev, y, B, world, timer):
              "frac": tflops / peak}
         if ref_dec is None:
             ref_dec, ref_lg = d0, l0
+            r["median_abs_logit"] = l0.abs().median().item()
         else:
             same = (d0 == ref_dec).all(1)
             r["cw_agreement_vs_fp32"] = same.float().mean().item()
-            r["max_logit_diff_vs_fp32_on_agreeing_cw"] = (l0[same] - ref_lg[same]).abs().max().item()
+            dl = (l0[same] - ref_lg[same]).abs()
+            r["max_logit_diff_vs_fp32_on_agreeing_cw"] = dl.max().item()
+            # relative to max(1, |logit|): trained logits reach O(10-100), where fp32 itself resolves ~1e-5
+            r["max_rel_logit_diff_vs_fp32_on_agreeing_cw"] = (dl / ref_lg[same].abs().clamp_min(1.0)).max().item()
         res[prec] = r
     f = res["fp32"]
     return {"value": f["value"], "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": f["avg_launch_ms"],
