@@ -1118,6 +1118,15 @@ __device__ __forceinline__ void gemm16s(const f4* __restrict__ smem4, int g, con
     }
 }
 
+// (p_row0 + p_row1) + (p_row2 + p_row3) over the four 16-lane rows, the same in every lane (the order of
+// __shfl_xor 16 then 32) on v_permlane16_swap / v_permlane32_swap: VALU, no LDS round trip
+__device__ __forceinline__ float sum_rows16(float p) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+    const float s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+}
+
 __device__ __forceinline__ f4 fma4(float x, const f4& c, const f4& p) {
     return f4{fmaf(x, c[0], p[0]), fmaf(x, c[1], p[1]), fmaf(x, c[2], p[2]), fmaf(x, c[3], p[3])};
 }
@@ -1222,8 +1231,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a
 #pragma unroll
                 for (int i = 0; i < 4; ++i) part += wl[i] * h1[ht][i];
             }
-            part += __shfl_xor(part, 16, 64);
-            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            const float out = sum_rows16(part) + a.b_lin;
             const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
             float d;
             if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
@@ -1447,8 +1455,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                     const f4 wl = c4(G::WLIN, 3);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) part = fmaf(wl[i], h1[3][i], part);
-                    part += __shfl_xor(part, 16, 64);
-                    const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+                    const float out = sum_rows16(part) + a.b_lin;
                     const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
                     float d;
                     if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
@@ -1538,11 +1545,12 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
     wy_lo = (int64_t)(per / 8);
 }
 
-static int gru16_mode() {  // NPD_GRU16=0: the 32-codeword split kernels; 1: gru16_kernel; 2: gru16p_kernel (A/B)
+// NPD_GRU16=0: the 32-codeword split kernels; 1: gru16_kernel; 2 (default, measured best): gru16p_kernel (A/B)
+static int gru16_mode() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("NPD_GRU16");
-        v = (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+        v = (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
     }
     return v;
 }
