@@ -1545,19 +1545,303 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
     wy_lo = (int64_t)(per / 8);
 }
 
-// NPD_GRU16=0: the 32-codeword split kernels; 1: gru16_kernel; 2 (default, measured best): gru16p_kernel (A/B)
+// ---- 32-codeword pipelined variant (NPD_GRU16=3 A/B): the same pipeline on v_mfma_f32_32x32x16 at ONE wave per SIMD.
+// PMC of gru16_kernel (profiles/round3/pmc_gru16_summary.json): MFMA busy 0.46 and VALU active 0.57 of the SIMD's
+// cycles -- the two serialise.  A 32x32x16 MFMA leaves 24 of its 32 cycles free for the same wave's VALU issue
+// (a 16x16x32 leaves 8 of 16), so the update chunks of the previous tile fit beside the current tile's MFMAs.
+// Weights and the y projection use the 32-codeword split image (GeoB, build_image_bf); constants follow in the
+// 32x32 accumulator order: vector V, tile t (32 rows), lane half h, register i = row (i&3) + 8(i>>2) + 4h.
+struct Geo32 {
+    static constexpr int TT = 6, HT = 2, KB = 4;
+    static constexpr int IMG4 = 3 * TT * KB * 64;  // 16-B fragments per split image (= GeoB<64, 2, *>::IMG / 4)
+    static constexpr int OFF_C = 2 * IMG4 * 4;
+    static constexpr int C0L0 = OFF_C, C1L0 = OFF_C + 192, BHN0 = OFF_C + 384, C0L1 = OFF_C + 448,
+                         BHN1 = OFF_C + 640, WLIN = OFF_C + 704, TOTAL = OFF_C + 768;
+};
+
+template <int SPLIT>
+struct Upd16 {
+    f16v er, ez, en, z;
+    template <int C>
+    __device__ __forceinline__ void step(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
+        constexpr float acc = SplitT<SPLIT>::kAcc;
+        constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+        constexpr int i = C / 3, st = C % 3;
+        if constexpr (st == 0) {
+            er[i] = __builtin_amdgcn_exp2f(c1 * ar[i]);
+            ez[i] = __builtin_amdgcn_exp2f(c1 * az[i]);
+        } else if constexpr (st == 1) {
+            const float r = __builtin_amdgcn_rcpf(1.0f + er[i]);
+            z[i] = __builtin_amdgcn_rcpf(1.0f + ez[i]);
+            en[i] = __builtin_amdgcn_exp2f(c2 * (ain[i] + ahn[i] * r));
+        } else {
+            const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + en[i]), -1.0f);
+            h[i] = (h[i] - nn) * z[i] + nn;
+        }
+    }
+};
+
+// B fragment q = 2t + s of a state: registers 8s .. 8s + 7 of tile t
+template <int SPLIT>
+__device__ __forceinline__ void split_q(const f16v (&h)[2], int q, typename SplitT<SPLIT>::V (&hi)[4],
+                                        typename SplitT<SPLIT>::V (&lo)[4]) {
+    using S = SplitT<SPLIT>;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = h[q >> 1][8 * (q & 1) + j] * S::kIn;
+        const typename S::E b = (typename S::E)v;
+        hi[q][j] = b;
+        if (S::kLo) lo[q][j] = (typename S::E)(v - (float)b);
+    }
+}
+
+__device__ __forceinline__ f16v fma16v(float x, const f16v& c, const f16v& p) {
+    f16v r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = fmaf(x, c[i], p[i]);
+    return r;
+}
+
+// acc[u] += W_g[32-row tile t[u]] . state over the 4 K steps (fragments of step q+1 loaded beside step q's MFMAs);
+// work chunks C0 .. C0 + NCH - 1 spread over the 4 NU MFMA triples, one sched_barrier-fenced region per triple
+template <int SPLIT, int NU, int C0, int NCH, typename Work>
+__device__ __forceinline__ void gemm32i(const f4* __restrict__ smem4, int g, const int (&t)[NU], int lane,
+                                        f16v (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[4],
+                                        const typename SplitT<SPLIT>::V (&bl)[4], Work&& work) {
+    using G = Geo32;
+    using V = typename SplitT<SPLIT>::V;
+    constexpr int NT = 4 * NU;
+    V ah[2][NU], al[2][NU];
+    auto load = [&](int q, int b) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int idx = ((g * G::TT + t[u]) * G::KB + q) * 64 + lane;
+            ah[b][u] = __builtin_bit_cast(V, smem4[idx]);
+            if (SplitT<SPLIT>::kLo) al[b][u] = __builtin_bit_cast(V, smem4[G::IMG4 + idx]);
+        }
+    };
+    load(0, 0);
+    static_for<0, 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if constexpr (q + 1 < 4) load(q + 1, (q + 1) & 1);
+        asm volatile("" ::: "memory");  // loop-invariant LDS reads stay in the step loop, one K step ahead
+        static_for<0, NU>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            constexpr int tr = q * NU + u;
+            acc[u] = mfma16(ah[q & 1][u], bh[q], acc[u]);
+            if (SplitT<SPLIT>::kLo) {
+                acc[u] = mfma16(ah[q & 1][u], bl[q], acc[u]);
+                acc[u] = mfma16(al[q & 1][u], bh[q], acc[u]);
+            }
+            static_for<C0 + NCH * tr / NT, C0 + NCH * (tr + 1) / NT>([&](auto cc) { work(cc); });
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    });
+}
+
+#define NPD_GRU32_WPB 4
+template <int SPLIT>
+__global__ __launch_bounds__(64 * NPD_GRU32_WPB) void gru32p_kernel(const ArgsB a) {
+    using G = Geo32;
+    using S = SplitT<SPLIT>;
+    using V = typename S::V;
+    using E = typename S::E;
+    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
+    const float* smem = reinterpret_cast<const float*>(smem4);
+    {
+        const f4* src = reinterpret_cast<const f4*>(a.img);
+        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int half = lane >> 5;
+    const int col = lane & 31;
+    const int N = a.N;
+    const int64_t ntiles = (a.B + 31) / 32;
+    // this lane's 16 accumulator-row values of 32-row tile t of a constant vector
+    auto c16 = [&](int off, int t) -> f16v {
+        const f4* p = reinterpret_cast<const f4*>(smem + off + (2 * t + half) * 16);
+        const f4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        return f16v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                    x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+    };
+    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    constexpr int T0[3] = {0, 2, 4};  // hidden tile 0: r, z, n rows
+    constexpr int T1[3] = {1, 3, 5};
+    auto nowork = [](auto) {};
+
+    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU32_WPB + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * NPD_GRU32_WPB) {
+        const int64_t cw = tile * 32 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        f16v P[G::TT];
+#pragma unroll
+        for (int t = 0; t < G::TT; ++t) P[t] = c16(G::C0L0, t);
+        {
+            const float* yr = a.y + cwc * N;
+            const int nq = N / 16;
+            for (int q = 0; q < nq; ++q) {
+                const f4 y0 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half);
+                const f4 y1 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half + 4);
+                V yh, yl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
+                    yh[j] = (E)v;
+                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
+                }
+#pragma unroll
+                for (int t = 0; t < G::TT; ++t) {
+                    const V wh = __builtin_bit_cast(V, a.wy[(t * nq + q) * 64 + lane]);
+                    P[t] = mfma16(wh, yh, P[t]);
+                    if (S::kLo) {
+                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nq + q) * 64 + lane]);
+                        P[t] = mfma16(wh, yl, P[t]);
+                        P[t] = mfma16(wl, yh, P[t]);
+                    }
+                }
+            }
+        }
+        f16v h0[2] = {zero, zero}, h1[2] = {zero, zero};
+        V fh[4], fl[4], gh[4], gl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            split_q<SPLIT>(h0, q, fh, fl);
+            split_q<SPLIT>(h1, q, gh, gl);
+        }
+        float xb = 1.0f;
+        // P enters the r / z accumulators as the first MFMA's C operand (no VALU read of P); the x_i column is
+        // added after the GEMM
+        f16v a0[3] = {P[0], P[2], c16(G::BHN0, 0)};
+        gemm32i<SPLIT, 3, 0, 0>(smem4, 0, T0, lane, a0, fh, fl, nowork);
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            Upd16<SPLIT> u;
+            // ================= layer 0: finish hidden tile 0, then tile 1 beside tile 0's update
+            const f16v ap0 = fma16v(xb, c16(G::C1L0, 0), a0[0]);
+            const f16v ap1 = fma16v(xb, c16(G::C1L0, 2), a0[1]);
+            const f16v ap2 = a0[2];
+            const f16v ain0 = fma16v(xb, c16(G::C1L0, 4), P[4]);
+            f16v acc[3] = {P[1], P[3], c16(G::BHN0, 1)};
+            gemm32i<SPLIT, 3, 0, 48>(smem4, 0, T1, lane, acc, fh, fl, [&](auto cc) {
+                u.template step<decltype(cc)::value>(h0[0], ap0, ap1, ain0, ap2);
+            });
+            acc[0] = fma16v(xb, c16(G::C1L0, 1), acc[0]);
+            acc[1] = fma16v(xb, c16(G::C1L0, 3), acc[1]);
+            const f16v ain1 = fma16v(xb, c16(G::C1L0, 5), P[5]);
+            // ================= layer 1, tile 0: W_hh1 h1 beside h0 tile 1's update and the h0' split
+            f16v b[3] = {c16(G::C0L1, 0), c16(G::C0L1, 2), c16(G::BHN1, 0)};
+            gemm32i<SPLIT, 3, 0, 52>(smem4, 2, T0, lane, b, gh, gl, [&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c < 48) u.template step<c>(h0[1], acc[0], acc[1], ain1, acc[2]);
+                else split_q<SPLIT>(h0, c - 48, fh, fl);
+            });
+            f16v bi[3] = {b[0], b[1], c16(G::C0L1, 4)};
+            gemm32i<SPLIT, 3, 0, 0>(smem4, 1, T0, lane, bi, fh, fl, nowork);
+            // ================= layer 1, tile 1 beside h1 tile 0's update and its output partial sum
+            float part = 0.0f;
+            auto work1 = [&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c < 48) {
+                    u.template step<c>(h1[0], bi[0], bi[1], bi[2], b[2]);
+                } else {
+                    const f16v wl = c16(G::WLIN, 0);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) part = fmaf(wl[i], h1[0][i], part);
+                }
+            };
+            f16v bb[3] = {c16(G::C0L1, 1), c16(G::C0L1, 3), c16(G::BHN1, 1)};
+            gemm32i<SPLIT, 3, 0, 25>(smem4, 2, T1, lane, bb, gh, gl, work1);
+            f16v bbi[3] = {bb[0], bb[1], c16(G::C0L1, 5)};
+            gemm32i<SPLIT, 3, 25, 24>(smem4, 1, T1, lane, bbi, fh, fl, work1);
+            // ================= tail: next step's layer-0 tile-0 GEMM beside h1 tile 1's update, the output, the
+            // decision and the h1 split
+            a0[0] = P[0];
+            a0[1] = P[2];
+            a0[2] = c16(G::BHN0, 0);
+            gemm32i<SPLIT, 3, 0, 53>(smem4, 0, T0, lane, a0, fh, fl, [&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if constexpr (c < 48) {
+                    u.template step<c>(h1[1], bbi[0], bbi[1], bbi[2], bb[2]);
+                } else if constexpr (c == 48) {
+                    const f16v wl = c16(G::WLIN, 1);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) part = fmaf(wl[i], h1[1][i], part);
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+                    const float out = (__uint_as_float(r[0]) + __uint_as_float(r[1])) + a.b_lin;
+                    const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+                    float d;
+                    if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+                    else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+                    if (half == 0 && valid) {
+                        a.decoded[cw * N + jj] = d;
+                        if (a.logits) a.logits[cw * N + ii] = out;
+                    }
+                    const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+                    xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+                } else {
+                    split_q<SPLIT>(h1, c - 49, gh, gl);
+                }
+            });
+        }
+    }
+}
+
+// image of gru32p_kernel: the 32-codeword split weight images (build_image_bf) + constants in 32x32 row order
+template <int SPLIT>
+static void build_image32(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
+                          int64_t& wy_lo) {
+    using G = Geo32;
+    std::vector<float> imgB, img16, wy16;
+    float b_lin = 0.0f;
+    build_image_bf<64, 2, SPLIT>(W, N, onehot, imgB, wy, b_lin, wy_lo);
+    int64_t dummy = 0;
+    build_image16<SPLIT>(W, N, onehot, img16, wy16, dummy);  // its constants (row-major) are reused
+    img.assign(G::TOTAL, 0.0f);
+    const int nw = (int)imgB.size() < G::OFF_C ? (int)imgB.size() : G::OFF_C;  // plain bf16: no lo image
+    for (int i = 0; i < nw; ++i) img[i] = imgB[i];
+    const int vec[6][2] = {{G::C0L0, Geo16::C0L0}, {G::C1L0, Geo16::C1L0}, {G::BHN0, Geo16::BHN0},
+                           {G::C0L1, Geo16::C0L1}, {G::BHN1, Geo16::BHN1}, {G::WLIN, Geo16::WLIN}};
+    const int rows[6] = {192, 192, 64, 192, 64, 64};
+    for (int v = 0; v < 6; ++v)
+        for (int t = 0; t < rows[v] / 32; ++t)
+            for (int h = 0; h < 2; ++h)
+                for (int i = 0; i < 16; ++i)
+                    img[vec[v][0] + (2 * t + h) * 16 + i] = img16[vec[v][1] + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h];
+}
+
+// NPD_GRU16=0: the 32-codeword split kernels; 1: gru16_kernel; 2 (default, measured best): gru16p_kernel;
+// 3: gru32p_kernel (A/B)
 static int gru16_mode() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("NPD_GRU16");
-        v = (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
+        v = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
     }
     return v;
 }
 static bool gru16_enabled() { return gru16_mode() != 0; }
 
 template <int SPLIT>
+static int launch32p(const ArgsB& a, hipStream_t s) {
+    auto kern = gru32p_kernel<SPLIT>;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    const int64_t tiles = (a.B + 31) / 32;
+    const int64_t wgs = (tiles + NPD_GRU32_WPB - 1) / NPD_GRU32_WPB;
+    const int grid = grid_for(wgs, 1, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU32_WPB), (size_t)Geo32::TOTAL * 4, s, a);
+    return launch_check("gru32p_kernel launch");
+}
+
+template <int SPLIT>
 static int launch16(const ArgsB& a, hipStream_t s) {
+    if (gru16_mode() == 3) return launch32p<SPLIT>(a, s);
     auto kern = gru16_mode() == 2 ? gru16p_kernel<SPLIT> : gru16_kernel<SPLIT>;
     static bool attr = false;
     if (!attr) {
@@ -1838,7 +2122,11 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     g->wy_lo = wy_lo;
     std::vector<float> img16, wy16;
     if (precision != 0 && F == 64 && layers == 2 && N % 32 == 0) {
-        if (precision == 1) gru::build_image16<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        if (gru::gru16_mode() == 3) {
+            if (precision == 1) gru::build_image32<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
+            else if (precision == 3) gru::build_image32<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
+            else gru::build_image32<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        } else if (precision == 1) gru::build_image16<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
         else if (precision == 3) gru::build_image16<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
         else gru::build_image16<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
     }
