@@ -33,6 +33,7 @@ struct npd_gru {
     float* img16;  // 16-codeword split kernel's image (F = 64, 2 layers, split precisions), or NULL
     float* wy16;
     int64_t wy16_lo;
+    int split16;   // its SplitT variant
 };
 
 namespace npd {
@@ -436,15 +437,20 @@ static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
 
-// SPLIT: 1 = bf16, 3 = bf16 hi + lo, 4 = fp16 hi + lo (scaled)
+// SPLIT: 1 = bf16, 3 = bf16 hi + lo, 4 = fp16 hi + lo (scaled), 5 = fp16 hi + lo, unscaled, gate constants folded
+// into the weights (16-codeword kernels only, see build_image16)
 template <int SPLIT>
 struct SplitT {
     static constexpr bool kLo = SPLIT >= 3;
-    static constexpr bool kF16 = SPLIT == 4;
+    static constexpr bool kF16 = SPLIT >= 4;
+    static constexpr bool kFold = SPLIT == 5;  // accumulators hold -log2(e) a (r, z rows) / -2 log2(e) a (n rows)
     using V = std::conditional_t<kF16, hf8, bf8>;
     using E = std::conditional_t<kF16, _Float16, __bf16>;
-    static constexpr float kIn = kF16 ? 256.0f : 1.0f;           // B-operand scale (states, y)
-    static constexpr float kAcc = kF16 ? 1.0f / 65536.0f : 1.0f;  // accumulator -> value
+    static constexpr float kIn = SPLIT == 4 ? 256.0f : 1.0f;           // B-operand scale (states, y)
+    static constexpr float kAcc = SPLIT == 4 ? 1.0f / 65536.0f : 1.0f;  // accumulator -> value
+    // exp2 arguments of sigmoid(a) = 1 / (1 + 2^(c1 a)) and tanh(x) = 2 / (1 + 2^(c2 x)) - 1 from the accumulators
+    static constexpr float kC1 = kFold ? 1.0f : -1.44269504088896340736f * kAcc;
+    static constexpr float kC2 = kFold ? 1.0f : -2.88539008177792681472f * kAcc;
 };
 
 template <int F, int L, int SPLIT>
@@ -487,8 +493,7 @@ __device__ __forceinline__ f16v mfma16(const hf8& a, const hf8& b, const f16v& c
 template <int SPLIT>
 __device__ __forceinline__ void gru_update_fast(f16v& h, const f16v& ar, const f16v& az, const f16v& ain,
                                                 const f16v& ahn) {
-    constexpr float acc = SplitT<SPLIT>::kAcc;
-    constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+    constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
@@ -710,8 +715,7 @@ __device__ __forceinline__ void mfma_frags(f16v (&acc)[NT], const typename Split
 template <int SPLIT>
 __device__ __forceinline__ void update_elems(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn,
                                              int e0, int e1) {
-    constexpr float acc = SplitT<SPLIT>::kAcc;
-    constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+    constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
 #pragma unroll
     for (int i = e0; i < e1; ++i) {
         const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
@@ -918,11 +922,11 @@ static float f16_to_f(uint16_t b) {
     memcpy(&h, &b, 2);
     return (float)h;
 }
-// 16-bit split of v: SPLIT 4 -> fp16 of v * 2^8; else bf16 of v
+// 16-bit split of v: SPLIT 4 -> fp16 of v * 2^8; SPLIT 5 -> fp16 of v (lo may be subnormal); else bf16 of v
 template <int SPLIT>
 static void split16(float v, uint16_t& hi, uint16_t& lo) {
-    if (SPLIT == 4) {
-        const float s = v * 256.0f;
+    if (SPLIT >= 4) {
+        const float s = SPLIT == 4 ? v * 256.0f : v;
         hi = f16_rne(s);
         lo = f16_rne(s - f16_to_f(hi));
     } else {
@@ -1062,8 +1066,7 @@ __device__ __forceinline__ f4 mfma16s(const bf8& a, const bf8& b, const f4& c) {
 
 template <int SPLIT>
 __device__ __forceinline__ void update4(f4& h, const f4& ar, const f4& az, const f4& ain, const f4& ahn) {
-    constexpr float acc = SplitT<SPLIT>::kAcc;
-    constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+    constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
@@ -1258,8 +1261,7 @@ struct Upd4 {
     f4 er, ez, en, z;
     template <int C>
     __device__ __forceinline__ void step(f4& h, const f4& ar, const f4& az, const f4& ain, const f4& ahn) {
-        constexpr float acc = SplitT<SPLIT>::kAcc;
-        constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+        constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
         constexpr int i = C / 3, st = C % 3;
         if constexpr (st == 0) {
             er[i] = __builtin_amdgcn_exp2f(c1 * ar[i]);
@@ -1496,6 +1498,8 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
     const float* wlin = p;
     img.assign(G::TOTAL, 0.0f);
     const float* mats[3] = {whh[0], wih[1], whh[1]};
+    // SPLIT 5: every gate row pre-multiplied by its exp2 constant (r, z: -log2 e; n: -2 log2 e; one fp32 rounding)
+    auto fold = [&](int row) { return SPLIT == 5 ? (row < 2 * F ? -1.44269504088896340736f : -2.88539008177792681472f) : 1.0f; };
     uint16_t* u16 = reinterpret_cast<uint16_t*>(img.data());
     for (int g = 0; g < G::NG; ++g)
         for (int t = 0; t < G::RT; ++t)
@@ -1505,7 +1509,7 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
                         const int row = 16 * t + (l & 15);
                         const int hid = 16 * (2 * kb + (j >> 2)) + 4 * (l >> 4) + (j & 3);
                         uint16_t hi, lo;
-                        split16<SPLIT>(mats[g][(size_t)row * F + hid], hi, lo);
+                        split16<SPLIT>(fold(row) * mats[g][(size_t)row * F + hid], hi, lo);
                         const size_t e = ((((size_t)(g * G::RT + t) * G::KB + kb) * 64 + l) * 8 + j);
                         u16[e] = hi;
                         if (SPLIT >= 3) u16[(size_t)G::IMG4 * 8 + e] = lo;
@@ -1517,13 +1521,13 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
         // x_i enters as c0 + x_i c1 (one-hot: columns N, N + 1 -> c0 = w_N, c1 = w_{N+1} - w_N; else c1 = w_N)
         const float c0x = onehot ? col(row, N) : 0.0f;
         const float c1x = onehot ? col(row, N + 1) - col(row, N) : col(row, N);
-        img[G::C0L0 + row] = kc * (rz ? bih[0][row] + bhh[0][row] + c0x : bih[0][row] + c0x);
-        img[G::C1L0 + row] = kc * c1x;
-        img[G::C0L1 + row] = kc * (rz ? bih[1][row] + bhh[1][row] : bih[1][row]);
+        img[G::C0L0 + row] = fold(row) * (kc * (rz ? bih[0][row] + bhh[0][row] + c0x : bih[0][row] + c0x));
+        img[G::C1L0 + row] = fold(row) * (kc * c1x);
+        img[G::C0L1 + row] = fold(row) * (kc * (rz ? bih[1][row] + bhh[1][row] : bih[1][row]));
     }
     for (int j = 0; j < F; ++j) {
-        img[G::BHN0 + j] = kc * bhh[0][2 * F + j];
-        img[G::BHN1 + j] = kc * bhh[1][2 * F + j];
+        img[G::BHN0 + j] = fold(2 * F + j) * (kc * bhh[0][2 * F + j]);
+        img[G::BHN1 + j] = fold(2 * F + j) * (kc * bhh[1][2 * F + j]);
         img[G::WLIN + j] = wlin[j];
     }
     const int nkb = N / 32;
@@ -1537,7 +1541,7 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
                     const int row = 16 * t + (l & 15);
                     const int k = 32 * kb + 8 * (l >> 4) + j;
                     uint16_t hi, lo;
-                    split16<SPLIT>(col(row, k), hi, lo);
+                    split16<SPLIT>(fold(row) * col(row, k), hi, lo);
                     const size_t e = (((size_t)t * nkb + kb) * 64 + l) * 8 + j;
                     w16[e] = hi;
                     if (SPLIT >= 3) w16[per + e] = lo;
@@ -1564,8 +1568,7 @@ struct Upd16 {
     f16v er, ez, en, z;
     template <int C>
     __device__ __forceinline__ void step(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
-        constexpr float acc = SplitT<SPLIT>::kAcc;
-        constexpr float c1 = -1.44269504088896340736f * acc, c2 = -2.88539008177792681472f * acc;
+        constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
         constexpr int i = C / 3, st = C % 3;
         if constexpr (st == 0) {
             er[i] = __builtin_amdgcn_exp2f(c1 * ar[i]);
@@ -1839,9 +1842,21 @@ static int launch32p(const ArgsB& a, hipStream_t s) {
     return launch_check("gru32p_kernel launch");
 }
 
+// NPD_GRU_FOLD=0: the scaled fp16 split (SPLIT 4) instead of the folded one (SPLIT 5) in the 16-codeword kernels
+static bool gru_fold() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NPD_GRU_FOLD");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 template <int SPLIT>
 static int launch16(const ArgsB& a, hipStream_t s) {
-    if (gru16_mode() == 3) return launch32p<SPLIT>(a, s);
+    if constexpr (SPLIT != 5) {
+        if (gru16_mode() == 3) return launch32p<SPLIT>(a, s);
+    }
     auto kern = gru16_mode() == 2 ? gru16p_kernel<SPLIT> : gru16_kernel<SPLIT>;
     static bool attr = false;
     if (!attr) {
@@ -2122,11 +2137,13 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     g->wy_lo = wy_lo;
     std::vector<float> img16, wy16;
     if (precision != 0 && F == 64 && layers == 2 && N % 32 == 0) {
+        g->split16 = precision == 1 ? 3 : precision == 3 ? (gru::gru16_mode() != 3 && gru::gru_fold() ? 5 : 4) : 1;
         if (gru::gru16_mode() == 3) {
             if (precision == 1) gru::build_image32<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
             else if (precision == 3) gru::build_image32<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
             else gru::build_image32<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
         } else if (precision == 1) gru::build_image16<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        else if (g->split16 == 5) gru::build_image16<5>(weights, N, onehot, img16, wy16, g->wy16_lo);
         else if (precision == 3) gru::build_image16<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
         else gru::build_image16<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
     }
@@ -2197,9 +2214,10 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
             b.img = g->img16;
             b.wy = reinterpret_cast<const gru::f4*>(g->wy16);
             b.wy_lo = g->wy16_lo;
-            return g->precision == 1   ? gru::launch16<3>(b, s)
-                   : g->precision == 3 ? gru::launch16<4>(b, s)
-                                       : gru::launch16<1>(b, s);
+            return g->split16 == 3   ? gru::launch16<3>(b, s)
+                   : g->split16 == 5 ? gru::launch16<5>(b, s)
+                   : g->split16 == 4 ? gru::launch16<4>(b, s)
+                                     : gru::launch16<1>(b, s);
         }
 #define NPD_LBF(FF, LL)                                                                                   \
         return g->precision == 1   ? gru::launch_bf<FF, LL, 3>(g, b, s)                                     \
