@@ -10,6 +10,8 @@ rc=$?; echo "gru pytest rc=$rc"; tail -6 gpurun_out/pytest_gru.log; stop $rc
 timeout -k 10 200 python -u tools/gru_prec.py > gpurun_out/gru_prec.log 2>&1
 rc=$?; echo "gru_prec rc=$rc"; cat gpurun_out/gru_prec.log; stop $rc
 [ -n "$QUICK" ] && exit 0
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; stop $rc
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -8 gpurun_out/pytest_gpu.log; stop $rc
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1
