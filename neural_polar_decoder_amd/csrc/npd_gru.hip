@@ -1052,7 +1052,10 @@ static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
 struct Geo16 {
     static constexpr int RT = 12, KB = 2, NG = 3;    // 16-row gate tiles, 32-unit K blocks, weight matrices
     static constexpr int IMG4 = NG * RT * KB * 64;   // 16-B fragments per split image
-    static constexpr int OFF_C = 2 * IMG4 * 4;       // floats: constants after the hi and lo images
+    // fragment (matrix g, row tile t, K block kb, part p = hi / lo) of lane l at f4 index (((g RT + t) KB + kb) 2 + p) 64 + l:
+    // a matrix spans 48 KB, so every read of a GEMM is an immediate offset (< 64 KB) from one per-lane base
+    static constexpr int G_BYTES = RT * KB * 2 * 1024;
+    static constexpr int OFF_C = 2 * IMG4 * 4;       // floats: constants after the weight fragments
     static constexpr int C0L0 = OFF_C, C1L0 = OFF_C + 192, BHN0 = OFF_C + 384, C0L1 = OFF_C + 448,
                          BHN1 = OFF_C + 640, WLIN = OFF_C + 704, TOTAL = OFF_C + 768;
 };
@@ -1094,8 +1097,14 @@ __device__ __forceinline__ void split16s(const f4 (&h)[4], typename SplitT<SPLIT
 }
 
 // acc[u] += W_g[row tile t[u]] . state over both K blocks
+// LDS fragment of the 16-codeword image: wb = this lane's byte base of the matrix (laundered once per kernel)
+__device__ __forceinline__ f4 frag16(const f4* __restrict__ smem4, uint32_t wb, int t, int kb, int part) {
+    return *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(smem4) + wb +
+                                        ((t * Geo16::KB + kb) * 2 + part) * 1024);
+}
+
 template <int SPLIT, int NU>
-__device__ __forceinline__ void gemm16s(const f4* __restrict__ smem4, int g, const int (&t)[NU], int lane,
+__device__ __forceinline__ void gemm16s(const f4* __restrict__ smem4, uint32_t wb, const int (&t)[NU],
                                         f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
                                         const typename SplitT<SPLIT>::V (&bl)[2]) {
     using G = Geo16;
@@ -1105,9 +1114,8 @@ __device__ __forceinline__ void gemm16s(const f4* __restrict__ smem4, int g, con
         V ah[NU], al[NU];
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-            const int idx = ((g * G::RT + t[u]) * G::KB + kb) * 64 + lane;
-            ah[u] = __builtin_bit_cast(V, smem4[idx]);
-            if (SplitT<SPLIT>::kLo) al[u] = __builtin_bit_cast(V, smem4[G::IMG4 + idx]);
+            ah[u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 0));
+            if (SplitT<SPLIT>::kLo) al[u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 1));
         }
         asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
 #pragma unroll
@@ -1156,7 +1164,19 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a
     const int nkb = N / 32;
     const int64_t ntiles = (a.B + 15) / 16;
     // rows 4 g4 .. 4 g4 + 3 of 16-row tile t of a constant vector
-    auto c4 = [&](int off, int t) -> f4 { return *reinterpret_cast<const f4*>(smem + off + 16 * t + 4 * g4); };
+    // per-lane LDS byte bases, laundered so that every fragment / constant read is base + immediate offset
+    uint32_t wbs[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        uint32_t v = g * G::G_BYTES + lane * 16;
+        asm volatile("" : "+v"(v));
+        wbs[g] = v;
+    }
+    uint32_t cb = (G::OFF_C + 4 * g4) * 4;
+    asm volatile("" : "+v"(cb));
+    auto c4 = [&](int off, int t) -> f4 {
+        return *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(smem4) + cb + (off - G::OFF_C + 16 * t) * 4);
+    };
     const f4 zero = {0.f, 0.f, 0.f, 0.f};
 
     for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU16_WPB + wave; tile < ntiles;
@@ -1209,7 +1229,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a
                 const int T[3] = {ht, 4 + ht, 8 + ht};
                 f4 acc[3] = {fma4(xb, c4(G::C1L0, ht), P[ht]), fma4(xb, c4(G::C1L0, 4 + ht), P[4 + ht]),
                              c4(G::BHN0, ht)};
-                gemm16s<SPLIT, 3>(smem4, 0, T, lane, acc, fh, fl);
+                gemm16s<SPLIT, 3>(smem4, wbs[0], T, acc, fh, fl);
                 const f4 ain = fma4(xb, c4(G::C1L0, 8 + ht), P[8 + ht]);
                 update4<SPLIT>(h0[ht], acc[0], acc[1], ain, acc[2]);
             }
@@ -1221,9 +1241,9 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a
             for (int ht = 0; ht < 4; ++ht) {
                 const int T[3] = {ht, 4 + ht, 8 + ht};
                 f4 ai[3] = {c4(G::C0L1, ht), c4(G::C0L1, 4 + ht), c4(G::C0L1, 8 + ht)};
-                gemm16s<SPLIT, 3>(smem4, 1, T, lane, ai, fh, fl);
+                gemm16s<SPLIT, 3>(smem4, wbs[1], T, ai, fh, fl);
                 f4 ah[3] = {ai[0], ai[1], c4(G::BHN1, ht)};
-                gemm16s<SPLIT, 3>(smem4, 2, T, lane, ah, gh, gl);
+                gemm16s<SPLIT, 3>(smem4, wbs[2], T, ah, gh, gl);
                 update4<SPLIT>(h1[ht], ah[0], ah[1], ai[2], ah[2]);
             }
             // ================= output: Linear(F, 1), reduced over the four lane groups
@@ -1294,10 +1314,9 @@ __device__ __forceinline__ void split_kb(const f4 (&h)[4], int kb, typename Spli
 // acc[u] += W_g[row tile t[u]] . state (both K blocks); work(IC<c>) for chunks C0 .. C0 + NCH - 1 spread evenly
 // over the 2 NU MFMA triples, one sched_barrier-fenced region per triple
 template <int SPLIT, int NU, int C0, int NCH, typename Work>
-__device__ __forceinline__ void gemm16i(const f4* __restrict__ smem4, int g, const int (&t)[NU], int lane,
+__device__ __forceinline__ void gemm16i(const f4* __restrict__ smem4, uint32_t wb, const int (&t)[NU],
                                         f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
                                         const typename SplitT<SPLIT>::V (&bl)[2], Work&& work) {
-    using G = Geo16;
     using V = typename SplitT<SPLIT>::V;
     constexpr int NT = 2 * NU;
     V ah[2][NU], al[2][NU];
@@ -1305,9 +1324,8 @@ __device__ __forceinline__ void gemm16i(const f4* __restrict__ smem4, int g, con
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-            const int idx = ((g * G::RT + t[u]) * G::KB + kb) * 64 + lane;
-            ah[kb][u] = __builtin_bit_cast(V, smem4[idx]);
-            if (SplitT<SPLIT>::kLo) al[kb][u] = __builtin_bit_cast(V, smem4[G::IMG4 + idx]);
+            ah[kb][u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 0));
+            if (SplitT<SPLIT>::kLo) al[kb][u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 1));
         }
     asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
     static_for<0, NT>([&](auto trc) {
@@ -1343,7 +1361,19 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
     const int N = a.N;
     const int nkb = N / 32;
     const int64_t ntiles = (a.B + 15) / 16;
-    auto c4 = [&](int off, int t) -> f4 { return *reinterpret_cast<const f4*>(smem + off + 16 * t + 4 * g4); };
+    // per-lane LDS byte bases, laundered so that every fragment / constant read is base + immediate offset
+    uint32_t wbs[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        uint32_t v = g * G::G_BYTES + lane * 16;
+        asm volatile("" : "+v"(v));
+        wbs[g] = v;
+    }
+    uint32_t cb = (G::OFF_C + 4 * g4) * 4;
+    asm volatile("" : "+v"(cb));
+    auto c4 = [&](int off, int t) -> f4 {
+        return *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(smem4) + cb + (off - G::OFF_C + 16 * t) * 4);
+    };
     const f4 zero = {0.f, 0.f, 0.f, 0.f};
     constexpr int T0[3] = {0, 4, 8};
     auto nowork = [](auto) {};
@@ -1392,7 +1422,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
         float xb = 1.0f;
         // layer 0, hidden tile 0 of step 0: W_hh0 h0 part (the x_i column and P are added at the top of the step)
         f4 a0[3] = {zero, zero, c4(G::BHN0, 0)};
-        gemm16i<SPLIT, 3, 0, 0>(smem4, 0, T0, lane, a0, fh, fl, nowork);
+        gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[0], T0, a0, fh, fl, nowork);
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             Upd4<SPLIT> u;
@@ -1404,7 +1434,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                 const int T[3] = {ht, 4 + ht, 8 + ht};
                 f4 acc[3] = {fma4(xb, c4(G::C1L0, ht), P[ht]), fma4(xb, c4(G::C1L0, 4 + ht), P[4 + ht]),
                              c4(G::BHN0, ht)};
-                gemm16i<SPLIT, 3, 0, 12>(smem4, 0, T, lane, acc, fh, fl, [&](auto cc) {
+                gemm16i<SPLIT, 3, 0, 12>(smem4, wbs[0], T, acc, fh, fl, [&](auto cc) {
                     u.template step<decltype(cc)::value>(h0[ht - 1], ap[0], ap[1], ainp, ap[2]);
                 });
                 ainp = fma4(xb, c4(G::C1L0, 8 + ht), P[8 + ht]);
@@ -1413,13 +1443,13 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
             });
             // ================= layer 1, hidden tile 0: W_hh1 h1 beside h0 tile 3's update and the h0' split
             f4 b[3] = {c4(G::C0L1, 0), c4(G::C0L1, 4), c4(G::BHN1, 0)};
-            gemm16i<SPLIT, 3, 0, 14>(smem4, 2, T0, lane, b, gh, gl, [&](auto cc) {
+            gemm16i<SPLIT, 3, 0, 14>(smem4, wbs[2], T0, b, gh, gl, [&](auto cc) {
                 constexpr int c = decltype(cc)::value;
                 if constexpr (c < 12) u.template step<c>(h0[3], ap[0], ap[1], ainp, ap[2]);
                 else split_kb<SPLIT>(h0, c - 12, fh, fl);
             });
             f4 bi[3] = {b[0], b[1], c4(G::C0L1, 8)};
-            gemm16i<SPLIT, 3, 0, 0>(smem4, 1, T0, lane, bi, fh, fl, nowork);
+            gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[1], T0, bi, fh, fl, nowork);
             f4 q[4] = {bi[0], bi[1], bi[2], b[2]};  // r, z, in, hn of the previous layer-1 tile
             float part = 0.0f;
             static_for<1, 4>([&](auto htc) {
@@ -1436,9 +1466,9 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                         for (int i = 0; i < 4; ++i) part = fmaf(wl[i], h1[ht - 1][i], part);
                     }
                 };
-                gemm16i<SPLIT, 3, 0, 7>(smem4, 2, T, lane, bb, gh, gl, work);
+                gemm16i<SPLIT, 3, 0, 7>(smem4, wbs[2], T, bb, gh, gl, work);
                 f4 bbi[3] = {bb[0], bb[1], c4(G::C0L1, 8 + ht)};
-                gemm16i<SPLIT, 3, 7, 6>(smem4, 1, T, lane, bbi, fh, fl, work);
+                gemm16i<SPLIT, 3, 7, 6>(smem4, wbs[1], T, bbi, fh, fl, work);
                 q[0] = bbi[0];
                 q[1] = bbi[1];
                 q[2] = bbi[2];
@@ -1449,7 +1479,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
             a0[0] = zero;
             a0[1] = zero;
             a0[2] = c4(G::BHN0, 0);
-            gemm16i<SPLIT, 3, 0, 15>(smem4, 0, T0, lane, a0, fh, fl, [&](auto cc) {
+            gemm16i<SPLIT, 3, 0, 15>(smem4, wbs[0], T0, a0, fh, fl, [&](auto cc) {
                 constexpr int c = decltype(cc)::value;
                 if constexpr (c < 12) {
                     u.template step<c>(h1[3], q[0], q[1], q[2], q[3]);
@@ -1510,9 +1540,9 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
                         const int hid = 16 * (2 * kb + (j >> 2)) + 4 * (l >> 4) + (j & 3);
                         uint16_t hi, lo;
                         split16<SPLIT>(fold(row) * mats[g][(size_t)row * F + hid], hi, lo);
-                        const size_t e = ((((size_t)(g * G::RT + t) * G::KB + kb) * 64 + l) * 8 + j);
+                        const size_t e = (((((size_t)(g * G::RT + t) * G::KB + kb) * 2) * 64 + l) * 8 + j);
                         u16[e] = hi;
-                        if (SPLIT >= 3) u16[(size_t)G::IMG4 * 8 + e] = lo;
+                        if (SPLIT >= 3) u16[e + 64 * 8] = lo;
                     }
     const float kc = SPLIT == 4 ? 65536.0f : 1.0f;
     auto col = [&](int row, int k) { return wih[0][(size_t)row * Din + k]; };
