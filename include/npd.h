@@ -221,7 +221,8 @@ int npd_count_errors_masked(const float* ref, const float* hat, const int64_t* m
  * weights: host fp32, packed per layer l = 0..layers-1 as
  *   weight_ih_l (3F, Din_l) | weight_hh_l (3F, F) | bias_ih_l (3F) | bias_hh_l (3F),
  * then linear.weight (F) | linear.bias (1); Din_0 = N + 2 (onehot) or N + 1, Din_l = F for l > 0.
- * precision: 0 = fp32 (default, exact fp32 FMA chains), 1 = bf16x3 split, 2 = bf16.
+ * precision: 0 = fp32 (default, exact fp32 FMA chains), 1 = bf16x3 split, 2 = bf16, 3 = fp16x3 split (hi + lo fp16
+ * parts, three products per multiply, fp32 accumulation: held to the fp32 path's tolerance; F <= 64).
  */
 int npd_gru_create(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
                    npd_gru** out);
