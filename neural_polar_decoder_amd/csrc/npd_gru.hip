@@ -34,6 +34,7 @@ struct npd_gru {
     float* wy16;
     int64_t wy16_lo;
     int split16;   // its SplitT variant
+    int fold32;    // fp32 F <= 64 image with the gate exp2 constants folded in (gru_decode_kernel<..., true>)
 };
 
 namespace npd {
@@ -147,6 +148,9 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v exp2_2(f2v x) { return f2v{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
 __device__ __forceinline__ f2v rcp_2(f2v x) { return f2v{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
 
+// FOLD: the image's gate rows were pre-multiplied by their exp2 constants (build_image(..., fold)): the accumulators
+// already hold -log2(e) a (r, z) and -2 log2(e) a (n), so no scaling multiply per gate
+template <bool FOLD = false>
 __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
 #if NPD_GRU_PRECISE_GATES
 #pragma unroll
@@ -158,15 +162,21 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
     }
 #else
     const f2v one = {1.0f, 1.0f};
-    const f2v ml2e = {-1.44269504088896340736f, -1.44269504088896340736f};
     const f2v two = {2.0f, 2.0f};
-    const f2v m2l2e = {-2.88539008177792681472f, -2.88539008177792681472f};  // (2x)(-log2 e) == x(-2 log2 e), both exact scalings
+    // (2x)(-log2 e) == x(-2 log2 e), both exact scalings
+    constexpr float k1 = FOLD ? 1.0f : -1.44269504088896340736f, k2 = FOLD ? 1.0f : -2.88539008177792681472f;
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
-        const f2v r = rcp_2(one + exp2_2(ml2e * f2v{ar[i], ar[i + 1]}));
-        const f2v z = rcp_2(one + exp2_2(ml2e * f2v{az[i], az[i + 1]}));
-        const f2v x = f2v{ain[i], ain[i + 1]} + f2v{ahn[i], ahn[i + 1]} * r;
-        const f2v s2 = rcp_2(one + exp2_2(m2l2e * x));
+        f2v er = f2v{ar[i], ar[i + 1]}, ez = f2v{az[i], az[i + 1]};
+        if constexpr (!FOLD) {
+            er = f2v{k1, k1} * er;
+            ez = f2v{k1, k1} * ez;
+        }
+        const f2v r = rcp_2(one + exp2_2(er));
+        const f2v z = rcp_2(one + exp2_2(ez));
+        f2v x = f2v{ain[i], ain[i + 1]} + f2v{ahn[i], ahn[i + 1]} * r;
+        if constexpr (!FOLD) x = f2v{k2, k2} * x;
+        const f2v s2 = rcp_2(one + exp2_2(x));
         const f2v nn = __builtin_elementwise_fma(two, s2, -one);
         const f2v hv = f2v{h[i], h[i + 1]};
         const f2v hn = (hv - nn) * z + nn;
@@ -187,7 +197,7 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
 #define NPD_GRU_BF_WPB 4
 #endif
 
-template <int F, int L, int WPB>
+template <int F, int L, int WPB, bool FOLD = false>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
 #pragma unroll
                 for (int j = 0; j < HT; ++j) {
                     const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
-                    gru_update(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
+                    gru_update<FOLD>(h0[j], acc[j], acc[HT + j], ain, acc[2 * HT + j]);
                 }
             }
             if constexpr (L == 2) {
@@ -278,7 +288,7 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
 #pragma unroll
                 for (int j = 0; j < HT; ++j) {
                     ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
-                    gru_update(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
+                    gru_update<FOLD>(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             }
             // ================= output: Linear(F, 1) on the top layer
@@ -313,7 +323,7 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
 // ---------------------------------------------------------------------------------- host image
 template <int F, int L>
 static void build_image(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
-                        float& b_lin) {
+                        float& b_lin, bool fold = false) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG, KS = G::KS;
     const int Din = N + (onehot ? 2 : 1);
@@ -335,13 +345,16 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
     img.assign(G::TOTAL, 0.0f);
     // main k-steps of the three images
     const float* mats[3] = {whh[0], L == 2 ? wih[1] : nullptr, L == 2 ? whh[1] : nullptr};
+    // fold: every gate row times its exp2 constant (r, z: -log2 e; n: -2 log2 e; one fp32 rounding), the kernel's
+    // gate nonlinearities then take the accumulators as they are (gru_update<true>)
+    auto fr = [&](int row) { return fold ? (row < 2 * F ? -1.44269504088896340736f : -2.88539008177792681472f) : 1.0f; };
     for (int g = 0; g < G::NG; ++g)
         for (int t = 0; t < TT; ++t)
             for (int s = 0; s < KS; ++s)
                 for (int l = 0; l < 64; ++l) {
                     const int row = 32 * t + (l & 31);
                     const int h = hid_of(s, l >> 5);
-                    img[((size_t)(g * TT + t) * KG + s / 4) * 256 + l * 4 + (s & 3)] = mats[g][(size_t)row * F + h];
+                    img[((size_t)(g * TT + t) * KG + s / 4) * 256 + l * 4 + (s & 3)] = fr(row) * mats[g][(size_t)row * F + h];
                 }
     // extra k-step A operands: column 0 pairs with B = 1, column 1 with B = x_i (layer 0) / 0 (layer 1)
     for (int t = 0; t < TT; ++t)
@@ -358,10 +371,10 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
                                   : wih[0][(size_t)row * Din + N])
                         : 0.0f;
             }
-            img[G::OFF_X + (0 * TT + t) * 64 + l] = v0;
+            img[G::OFF_X + (0 * TT + t) * 64 + l] = fr(row) * v0;
             if (L == 2) {
-                img[G::OFF_X + (1 * TT + t) * 64 + l] = kk == 0 ? (rz ? bih[1][row] + bhh[1][row] : bih[1][row]) : 0.0f;
-                img[G::OFF_X + (2 * TT + t) * 64 + l] = kk == 0 ? (rz ? 0.0f : bhh[1][row]) : 0.0f;
+                img[G::OFF_X + (1 * TT + t) * 64 + l] = fr(row) * (kk == 0 ? (rz ? bih[1][row] + bhh[1][row] : bih[1][row]) : 0.0f);
+                img[G::OFF_X + (2 * TT + t) * 64 + l] = fr(row) * (kk == 0 ? (rz ? 0.0f : bhh[1][row]) : 0.0f);
             }
         }
     for (int j = 0; j < HT; ++j)
@@ -371,7 +384,7 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             float v;
             if (kk == 0) v = bih[0][row] + (onehot ? wih[0][(size_t)row * Din + N] : 0.0f);
             else v = onehot ? wih[0][(size_t)row * Din + N + 1] - wih[0][(size_t)row * Din + N] : wih[0][(size_t)row * Din + N];
-            img[G::OFF_IN + j * 64 + l] = v;
+            img[G::OFF_IN + j * 64 + l] = fr(row) * v;
         }
     for (int hf = 0; hf < 2; ++hf)
         for (int t = 0; t < HT; ++t)
@@ -384,14 +397,14 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             for (int l = 0; l < 64; ++l) {
                 const int row = 32 * t + (l & 31);
                 const int k = s + (l >> 5) * (N / 2);
-                wy[((size_t)t * ng + s / 4) * 256 + l * 4 + (s & 3)] = wih[0][(size_t)row * Din + k];
+                wy[((size_t)t * ng + s / 4) * 256 + l * 4 + (s & 3)] = fr(row) * wih[0][(size_t)row * Din + k];
             }
 }
 
-template <int F, int L, int WPB>
+template <int F, int L, int WPB, bool FOLD>
 static int launch_w(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
-    auto kern = gru_decode_kernel<F, L, WPB>;
+    auto kern = gru_decode_kernel<F, L, WPB, FOLD>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -405,6 +418,16 @@ static int launch_w(const Args& a, hipStream_t s) {
     return launch_check("gru_decode_kernel launch");
 }
 
+// NPD_GRU_FOLD32=0: the fp32 F <= 64 kernel without the folded gate constants (A/B)
+static bool gru_fold32() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NPD_GRU_FOLD32");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 static int gru_waves() {
     static int w = -1;
     if (w < 0) {
@@ -416,8 +439,8 @@ static int gru_waves() {
 
 template <int F, int L>
 static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
-    (void)g;
-    return gru_waves() == 4 ? launch_w<F, L, 4>(a, s) : launch_w<F, L, 8>(a, s);
+    if (g->fold32) return gru_waves() == 4 ? launch_w<F, L, 4, true>(a, s) : launch_w<F, L, 8, true>(a, s);
+    return gru_waves() == 4 ? launch_w<F, L, 4, false>(a, s) : launch_w<F, L, 8, false>(a, s);
 }
 
 
@@ -2143,7 +2166,7 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     int64_t wy_lo = 0;
 #define NPD_BUILD(FF, LL)                                                                              \
     do {                                                                                               \
-        if (precision == 0) gru::build_image<FF, LL>(weights, N, onehot, img, wy, b_lin);              \
+        if (precision == 0) gru::build_image<FF, LL>(weights, N, onehot, img, wy, b_lin, gru::gru_fold32()); \
         else if (precision == 1) gru::build_image_bf<FF, LL, 3>(weights, N, onehot, img, wy, b_lin, wy_lo); \
         else if (precision == 3) gru::build_image_bf<FF, LL, 4>(weights, N, onehot, img, wy, b_lin, wy_lo); \
         else gru::build_image_bf<FF, LL, 1>(weights, N, onehot, img, wy, b_lin, wy_lo);               \
@@ -2163,6 +2186,7 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     if (!g) return fail(NPD_ENOMEM, "npd_gru_create: out of memory");
     memset(g, 0, sizeof(*g));
     g->N = N; g->F = F; g->layers = layers; g->onehot = onehot; g->precision = precision; g->b_lin = b_lin;
+    g->fold32 = precision == 0 && F <= 64 && gru::gru_fold32();
     g->img_floats = (int64_t)img.size();
     g->wy_lo = wy_lo;
     std::vector<float> img16, wy16;
