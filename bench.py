@@ -339,7 +339,12 @@ def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
     c16n = c16.cpu().numpy()
     flop_cw = gru_flop_per_cw(N_CODE, 64)
     tf = flop_cw * B / (ms / 1e3) / 1e12
+    tf16 = flop_cw * B / (ms16 / 1e3) / 1e12
     fp16x3 = {"value": world * len(snrs) * B / t16, "ms_per_step": t16 * 1e3, "gru_avg_launch_ms": ms16,
+              "roofline": {"bound": "mfma + valu issue (serialised on the SIMD: profiles/round3/pmc_gru16_summary.json)",
+                           "kernel": "gru16p_kernel (16-codeword waves, v_mfma_f32_16x16x32_f16, 3 products per multiply)",
+                           "achieved": tf16, "peak": 2516.6, "unit": "TFLOP/s", "frac": tf16 / 2516.6,
+                           "algorithmic_flop_per_cw": flop_cw},
               "gru_bit_errors_vs_fp32_path": [int(a) - int(b) for a, b in zip(c16n[:, 0], cg[:, 0])],
               "gru_block_errors_vs_fp32_path": [int(a) - int(b) for a, b in zip(c16n[:, 1], cg[:, 1])],
               "note": "GRU on the scaled hi+lo fp16 split (3 v_mfma_f32_32x32x16_f16 products per multiply, fp32 "
