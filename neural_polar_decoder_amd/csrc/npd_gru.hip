@@ -1062,9 +1062,11 @@ static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
 // above need ~500 registers (P, both states, the gate accumulators): one wave per SIMD, and a step is one serial
 // chain (layer-0 GEMM -> update -> split -> layer-1 GEMM -> update -> output -> decision) that leaves the MFMA pipe
 // idle while the wave does its VALU work.  Here a wave owns 16 codewords on v_mfma_f32_16x16x32_{f16,bf16} (the same
-// FLOP per cycle as 32x32x16), so every register array halves and TWO waves share each SIMD: a 16-bit MFMA holds its
-// SIMD's vector issue for only 8 of its 16 cycles (MI355X_MICROARCH.md), so one wave's gate updates, splits and
-// output issue in the other wave's MFMA gaps.
+// FLOP per cycle as 32x32x16), so every register array halves and TWO waves share each SIMD, hiding each other's
+// LDS and dependency latencies.  (They do not hide each other's VALU work behind MFMAs: measured, an fp16 MFMA wave
+// and an FMA wave on one SIMD take the sum of their times, profiles/round3/coissue.txt; PMC: MFMA busy + VALU
+// active ~ all SIMD cycles.  Hence the VALU trims below: no fp32 k-step MFMAs, folded gate constants, permlane
+// reductions, immediate-offset LDS reads.)
 // 16x16x32 maps: lane l = 16 g + c holds D[row 4g + i][codeword c] (i = 0..3), A[row c][k 8g + j], B[k 8g + j][col c].
 // Hidden units form 16-row tiles ht = 0..3; K block kb (32 units) is tiles 2kb, 2kb + 1, with MFMA k index 8g + j
 // <-> hidden unit 16 (2kb + (j >> 2)) + 4g + (j & 3): an updated state tile converts register for register into the
