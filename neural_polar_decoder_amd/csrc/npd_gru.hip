@@ -67,7 +67,10 @@ struct Geo {
     static constexpr int OFF_X = NG * G_SIZE;        // extra k-step A operands [g][t][64]
     static constexpr int OFF_IN = OFF_X + NG * TT * 64;  // layer-0 n-gate input extra [HT][64]
     static constexpr int OFF_WL = OFF_IN + HT * 64;      // linear weights [half][HT][16]
-    static constexpr int TOTAL = OFF_WL + 2 * HT * 16;
+    // bias vectors in accumulator-register order (tile, lane half, register i = row (i&3) + 8(i>>2) + 4 half) for the
+    // folded kernel's accumulator initialisation: [b_hh0 n: HT tiles][layer-1 c0: TT tiles][b_hh1 n: HT tiles]
+    static constexpr int OFF_CV = OFF_WL + 2 * HT * 16;
+    static constexpr int TOTAL = OFF_CV + (2 * HT + TT) * 32;
 };
 
 // hidden unit fed by lane half `kk` at k-step s (accumulator row map of the 32x32 MFMA tile)
@@ -197,7 +200,7 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
 #define NPD_GRU_BF_WPB 4
 #endif
 
-template <int F, int L, int WPB, bool FOLD = false>
+template <int F, int L, int WPB, bool FOLD = false, bool BINIT = false>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
@@ -215,6 +218,13 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     const int N = a.N;
     const int64_t ntiles = (a.B + 31) / 32;
     const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // this lane's 16 accumulator-row values of a bias vector tile at float offset `off` (Geo::OFF_CV region)
+    auto cvec = [&](int off) -> f16v {
+        const f4* p = reinterpret_cast<const f4*>(smem + off + half * 16);
+        const f4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        return f16v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                    x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+    };
 
     for (int64_t tile = (int64_t)blockIdx.x * WPB + wave; tile < ntiles; tile += (int64_t)gridDim.x * WPB) {
         const int64_t cw = tile * 32 + col;
@@ -259,10 +269,11 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
 #pragma unroll
                 for (int t = 0; t < 2 * HT; ++t) acc[t] = P[t];
 #pragma unroll
-                for (int t = 2 * HT; t < TT; ++t) acc[t] = zero;
+                for (int t = 2 * HT; t < TT; ++t) acc[t] = BINIT ? cvec(G::OFF_CV + (t - 2 * HT) * 32) : zero;
                 gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
+                // the [1, x_i] k-step: every tile, or (BINIT: hn tiles start from their bias) the r, z tiles only
 #pragma unroll
-                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
+                for (int t = 0; t < (BINIT ? 2 * HT : TT); ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, acc[t]);
 #pragma unroll
                 for (int j = 0; j < HT; ++j) {
                     const f16v ain = mfma(smem[G::OFF_IN + j * 64 + lane], xbe, P[2 * HT + j]);
@@ -273,21 +284,23 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                 // ================= layer 1: acc1 = W_ih1 h0' (+ W_hh1 h1 on r,z rows); ahn = W_hh1_n h1
                 f16v acc1[TT];
 #pragma unroll
-                for (int t = 0; t < TT; ++t) acc1[t] = zero;
+                for (int t = 0; t < TT; ++t) acc1[t] = BINIT ? cvec(G::OFF_CV + (HT + t) * 32) : zero;
                 gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
+                if constexpr (!BINIT) {
 #pragma unroll
-                for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
+                    for (int t = 0; t < TT; ++t) acc1[t] = mfma(smem[G::OFF_X + (TT + t) * 64 + lane], one_or_zero, acc1[t]);
+                }
                 f16v arz[2 * HT];
 #pragma unroll
                 for (int t = 0; t < 2 * HT; ++t) arz[t] = acc1[t];
                 gemm_chain<TT, KG, 2 * HT, HT>(smem4, 2, 0, lane, arz, h1);
                 f16v ahn[HT];
 #pragma unroll
-                for (int j = 0; j < HT; ++j) ahn[j] = zero;
+                for (int j = 0; j < HT; ++j) ahn[j] = BINIT ? cvec(G::OFF_CV + (HT + TT + j) * 32) : zero;
                 gemm_chain<TT, KG, HT, HT>(smem4, 2, 2 * HT, lane, ahn, h1);
 #pragma unroll
                 for (int j = 0; j < HT; ++j) {
-                    ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
+                    if constexpr (!BINIT) ahn[j] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + j) * 64 + lane], one_or_zero, ahn[j]);
                     gru_update<FOLD>(h1[j], arz[j], arz[HT + j], acc1[2 * HT + j], ahn[j]);
                 }
             }
@@ -389,6 +402,24 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
     for (int hf = 0; hf < 2; ++hf)
         for (int t = 0; t < HT; ++t)
             for (int i = 0; i < 16; ++i) img[G::OFF_WL + (hf * HT + t) * 16 + i] = wlin[32 * t + (i & 3) + 8 * (i >> 2) + 4 * hf];
+    for (int v = 0; v < 2 * HT + TT; ++v)
+        for (int hf = 0; hf < 2; ++hf)
+            for (int i = 0; i < 16; ++i) {
+                const int r = (i & 3) + 8 * (i >> 2) + 4 * hf;
+                float val = 0.0f;
+                int row;
+                if (v < HT) {  // layer-0 hn bias
+                    row = 2 * F + 32 * v + r;
+                    val = bhh[0][row];
+                } else if (v < HT + TT) {  // layer-1 r, z (both biases) / in (b_ih) constants
+                    row = 32 * (v - HT) + r;
+                    val = L == 2 ? (row < 2 * F ? bih[1][row] + bhh[1][row] : bih[1][row]) : 0.0f;
+                } else {  // layer-1 hn bias
+                    row = 2 * F + 32 * (v - HT - TT) + r;
+                    val = L == 2 ? bhh[1][row] : 0.0f;
+                }
+                img[G::OFF_CV + (v * 2 + hf) * 16 + i] = fr(row) * val;
+            }
     // y projection: k-step s pairs y[s] (lanes 0-31) with y[s + N/2] (lanes 32-63)
     const int ng = N / 8;
     wy.assign((size_t)TT * ng * 256, 0.0f);
@@ -401,10 +432,10 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L, int WPB, bool FOLD>
+template <int F, int L, int WPB, bool FOLD, bool BINIT>
 static int launch_w(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
-    auto kern = gru_decode_kernel<F, L, WPB, FOLD>;
+    auto kern = gru_decode_kernel<F, L, WPB, FOLD, BINIT>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -428,6 +459,16 @@ static bool gru_fold32() {
     return v == 1;
 }
 
+// NPD_GRU_BINIT=1: biases as accumulator initialisation (Geo::OFF_CV) instead of the bias k-step MFMAs (A/B)
+static bool gru_binit() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("NPD_GRU_BINIT");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 static int gru_waves() {
     static int w = -1;
     if (w < 0) {
@@ -439,8 +480,9 @@ static int gru_waves() {
 
 template <int F, int L>
 static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
-    if (g->fold32) return gru_waves() == 4 ? launch_w<F, L, 4, true>(a, s) : launch_w<F, L, 8, true>(a, s);
-    return gru_waves() == 4 ? launch_w<F, L, 4, false>(a, s) : launch_w<F, L, 8, false>(a, s);
+    if (gru_waves() == 8) return g->fold32 ? launch_w<F, L, 8, true, false>(a, s) : launch_w<F, L, 8, false, false>(a, s);
+    if (g->fold32) return gru_binit() ? launch_w<F, L, 4, true, true>(a, s) : launch_w<F, L, 4, true, false>(a, s);
+    return gru_binit() ? launch_w<F, L, 4, false, true>(a, s) : launch_w<F, L, 4, false, false>(a, s);
 }
 
 

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop() { case $1 in 0|1) return 0;; *) echo "stopping after rc=$1"; exit $1;; esac; }
-timeout -k 10 300 python -u -m pytest tests/test_gru_gpu.py tests/test_trained_gru_gpu.py -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_gru_fold.log 2>&1
+env ${TESTENV:-NPD_X=0} timeout -k 10 300 python -u -m pytest tests/test_gru_gpu.py tests/test_trained_gru_gpu.py -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_gru_fold.log 2>&1
 rc=$?; echo "gru pytest rc=$rc"; tail -15 gpurun_out/pytest_gru_fold.log; stop $rc
 VAR=${VAR:-NPD_GRU_FOLD}
 for f in 1 0 1 0; do
