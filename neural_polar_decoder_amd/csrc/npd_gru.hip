@@ -459,12 +459,13 @@ static bool gru_fold32() {
     return v == 1;
 }
 
-// NPD_GRU_BINIT=1: biases as accumulator initialisation (Geo::OFF_CV) instead of the bias k-step MFMAs (A/B)
+// NPD_GRU_BINIT=0: bias k-step MFMAs instead of the biases as accumulator initialisation (Geo::OFF_CV; default,
+// measured 40.07 -> 39.70 ms per 2^20 Polar(64,32) words) (A/B)
 static bool gru_binit() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("NPD_GRU_BINIT");
-        v = (e && e[0] == '1') ? 1 : 0;
+        v = (e && e[0] == '0') ? 0 : 1;
     }
     return v == 1;
 }
