@@ -34,7 +34,6 @@ struct npd_gru {
     float* wy16;
     int64_t wy16_lo;
     int split16;   // its SplitT variant
-    int fold32;    // fp32 F <= 64 image with the gate exp2 constants folded in (gru_decode_kernel<..., true>)
 };
 
 namespace npd {
@@ -94,8 +93,6 @@ struct Args {
     uint32_t info[kMaxWords];
 };
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-
 __device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -130,17 +127,9 @@ __device__ __forceinline__ void gemm_chain(const f4* __restrict__ smem4, int g, 
     }
 }
 
-// Gate nonlinearities on the hardware transcendentals: sigmoid(x) = rcp(1 + exp2(-x log2 e)),
+// Gate nonlinearities on the hardware transcendentals (gru_update below): sigmoid(x) = rcp(1 + exp2(-x log2 e)),
 // tanh(x) = 2 sigmoid(2x) - 1 (v_exp_f32 / v_rcp_f32, ~1 ulp each; absolute error of tanh ~1e-7 near 0).
 // PyTorch's CPU kernels are not bit-reproducible either; the logit tolerance (tests) covers both.
-// NPD_GRU_PRECISE_GATES=1 selects the libm expf / tanhf forms instead.
-#ifndef NPD_GRU_PRECISE_GATES
-#define NPD_GRU_PRECISE_GATES 0
-#endif
-__device__ __forceinline__ float fast_sigmoid(float x) {
-    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896340736f * x));
-}
-__device__ __forceinline__ float fast_tanh(float x) { return fmaf(2.0f, fast_sigmoid(2.0f * x), -1.0f); }
 
 // PyTorch GRUCell update on one 32x32 tile pair: h = (h - n) * z + n,
 // r = sigmoid(a_r), z = sigmoid(a_z), n = tanh(a_in + r * a_hn)
@@ -155,15 +144,6 @@ __device__ __forceinline__ f2v rcp_2(f2v x) { return f2v{__builtin_amdgcn_rcpf(x
 // already hold -log2(e) a (r, z) and -2 log2(e) a (n), so no scaling multiply per gate
 template <bool FOLD = false>
 __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
-#if NPD_GRU_PRECISE_GATES
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float r = sigmoidf_(ar[i]);
-        const float z = sigmoidf_(az[i]);
-        const float nn = tanhf(ain[i] + ahn[i] * r);
-        h[i] = (h[i] - nn) * z + nn;
-    }
-#else
     const f2v one = {1.0f, 1.0f};
     const f2v two = {2.0f, 2.0f};
     // (2x)(-log2 e) == x(-2 log2 e), both exact scalings
@@ -186,22 +166,23 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
         h[i] = hn.x;
         h[i + 1] = hn.y;
     }
-#endif
 }
 
 // Waves per workgroup of the F <= 64 kernels: all share the workgroup's LDS copy of the weights.  8 waves
 // would put two on every SIMD (one wave's gate VALU work overlapping the other's MFMAs), but at <= 256
 // registers per wave the F = 64, 2-layer kernel spills (P, both states, the gate accumulators and the
 // weight look-ahead need ~300): measured 0.63 of the fp32 MFMA peak vs 0.77 with 4 waves.
-#ifndef NPD_GRU_WPB
-#define NPD_GRU_WPB 4   // default (measured: 8 waves spill 716 B/lane and run 0.63 vs 0.77 of peak); NPD_GRU_WAVES=8 A/B
-#endif
+#define NPD_GRU_WPB 4  // measured: 8 waves spill 716 B/lane and run 0.63 vs 0.77 of peak
 #ifndef NPD_GRU_BF_WPB
 #define NPD_GRU_BF_WPB 4
 #endif
 
-template <int F, int L, int WPB, bool FOLD = false, bool BINIT = false>
+// The image's gate rows carry their exp2 constants (build_image(..., fold = true)) and the biases initialise the
+// accumulators (Geo::OFF_CV): only layer 0's r, z tiles keep the [1, x_i] k-step.  Measured in round 3 (same box,
+// alternating, 2^20 Polar(64,32) words): folding 41.0 -> 40.3 ms, bias initialisation 40.07 -> 39.70 ms.
+template <int F, int L, int WPB = NPD_GRU_WPB>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
+    constexpr bool FOLD = true, BINIT = true;
     using G = Geo<F, L>;
     constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
     extern __shared__ __attribute__((aligned(16))) f4 smem4[];
@@ -432,10 +413,11 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L, int WPB, bool FOLD, bool BINIT>
-static int launch_w(const Args& a, hipStream_t s) {
+template <int F, int L>
+static int launch(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
-    auto kern = gru_decode_kernel<F, L, WPB, FOLD, BINIT>;
+    constexpr int WPB = NPD_GRU_WPB;
+    auto kern = gru_decode_kernel<F, L, WPB>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -448,44 +430,6 @@ static int launch_w(const Args& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WPB), lds, s, a);
     return launch_check("gru_decode_kernel launch");
 }
-
-// NPD_GRU_FOLD32=0: the fp32 F <= 64 kernel without the folded gate constants (A/B)
-static bool gru_fold32() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_GRU_FOLD32");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
-// NPD_GRU_BINIT=0: bias k-step MFMAs instead of the biases as accumulator initialisation (Geo::OFF_CV; default,
-// measured 40.07 -> 39.70 ms per 2^20 Polar(64,32) words) (A/B)
-static bool gru_binit() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_GRU_BINIT");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
-static int gru_waves() {
-    static int w = -1;
-    if (w < 0) {
-        const char* e = getenv("NPD_GRU_WAVES");
-        w = (e && atoi(e) == 4) ? 4 : (e && atoi(e) == 8) ? 8 : NPD_GRU_WPB;
-    }
-    return w;
-}
-
-template <int F, int L>
-static int launch(const npd_gru* g, const Args& a, hipStream_t s) {
-    if (gru_waves() == 8) return g->fold32 ? launch_w<F, L, 8, true, false>(a, s) : launch_w<F, L, 8, false, false>(a, s);
-    if (g->fold32) return gru_binit() ? launch_w<F, L, 4, true, true>(a, s) : launch_w<F, L, 4, true, false>(a, s);
-    return gru_binit() ? launch_w<F, L, 4, false, true>(a, s) : launch_w<F, L, 4, false, false>(a, s);
-}
-
 
 // =============================================================================== split 16-bit MFMA paths
 // precision 1 = bf16x3 split (a*b ~ ah*bh + ah*bl + al*bh, ~2^-16 relative per product),
@@ -746,223 +690,6 @@ __global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_decode_bf_kernel(cons
     }
 }
 
-// ---- F = 64, 2 layers, hidden-tile-grouped order (split paths).  A 16-bit MFMA holds its wave's vector issue
-// for only 8 of its 32 cycles (MI355X_MICROARCH.md), so a gate update issued beside MFMAs it does not depend on
-// costs little.  Each layer's GEMM is done per hidden tile j (its r, z and n rows: tiles j, HT + j, 2HT + j) and
-// the update of tile 0 is spread over tile 1's k-steps in source order (sched_barrier fences keep it there);
-// no accumulator lives longer than in the plain order.  Same operations per element as gru_decode_bf_kernel.
-template <int SPLIT, int NT>
-__device__ __forceinline__ void load_frags(const f4* __restrict__ smem4, int g, const int (&tl)[NT], int q, int lane,
-                                           typename SplitT<SPLIT>::V (&ah)[NT], typename SplitT<SPLIT>::V (&al)[NT]) {
-    using G = GeoB<64, 2, SPLIT>;
-    using V = typename SplitT<SPLIT>::V;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        ah[t] = __builtin_bit_cast(V, smem4[((g * G::TT + tl[t]) * G::KB + q) * 64 + lane]);
-        if (SplitT<SPLIT>::kLo) al[t] = __builtin_bit_cast(V, smem4[G::IMG / 4 + ((g * G::TT + tl[t]) * G::KB + q) * 64 + lane]);
-    }
-}
-
-template <int SPLIT, int NT>
-__device__ __forceinline__ void mfma_frags(f16v (&acc)[NT], const typename SplitT<SPLIT>::V (&ah)[NT],
-                                           const typename SplitT<SPLIT>::V (&al)[NT], const typename SplitT<SPLIT>::V& bh,
-                                           const typename SplitT<SPLIT>::V& bl) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        acc[t] = mfma16(ah[t], bh, acc[t]);
-        if (SplitT<SPLIT>::kLo) {
-            acc[t] = mfma16(ah[t], bl, acc[t]);
-            acc[t] = mfma16(al[t], bh, acc[t]);
-        }
-    }
-}
-
-// element pairs [p0, p1) of one hidden tile's GRU update (gru_update_fast's arithmetic, pair by pair)
-template <int SPLIT>
-__device__ __forceinline__ void update_elems(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn,
-                                             int e0, int e1) {
-    constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
-#pragma unroll
-    for (int i = e0; i < e1; ++i) {
-        const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
-        const float z = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * az[i]));
-        const float x = ain[i] + ahn[i] * r;
-        const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c2 * x)), -1.0f);
-        h[i] = (h[i] - nn) * z + nn;
-    }
-}
-
-template <int SPLIT>
-__global__ __launch_bounds__(64 * NPD_GRU_BF_WPB) void gru_grouped_kernel(const ArgsB a) {
-    using G = GeoB<64, 2, SPLIT>;
-    using S = SplitT<SPLIT>;
-    using V = typename S::V;
-    using E = typename S::E;
-    constexpr int TT = G::TT, HT = G::HT, KB = G::KB;
-    static_assert(HT == 2 && KB == 4, "F = 64");
-    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
-    const float* smem = reinterpret_cast<const float*>(smem4);
-    {
-        const f4* src = reinterpret_cast<const f4*>(a.img);
-        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int half = lane >> 5;
-    const int col = lane & 31;
-    const int N = a.N;
-    const int64_t ntiles = (a.B + 31) / 32;
-    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const float one_or_zero = half ? 0.0f : 1.0f;
-    constexpr int T0[3] = {0, HT, 2 * HT};      // hidden tile 0: r, z, n rows
-    constexpr int T1[3] = {1, HT + 1, 2 * HT + 1};
-
-    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU_BF_WPB + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * NPD_GRU_BF_WPB) {
-        const int64_t cw = tile * 32 + col;
-        const bool valid = cw < a.B;
-        const int64_t cwc = valid ? cw : a.B - 1;
-        f16v P[TT];
-#pragma unroll
-        for (int t = 0; t < TT; ++t) P[t] = zero;
-        {
-            const float* yr = a.y + cwc * N;
-            const int nq = N / 16;
-            for (int q = 0; q < nq; ++q) {
-                const f4 y0 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half);
-                const f4 y1 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half + 4);
-                V yh, yl;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
-                    yh[j] = (E)v;
-                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
-                }
-#pragma unroll
-                for (int t = 0; t < TT; ++t) {
-                    const V wh = __builtin_bit_cast(V, a.wy[(t * nq + q) * 64 + lane]);
-                    P[t] = mfma16(wh, yh, P[t]);
-                    if (S::kLo) {
-                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nq + q) * 64 + lane]);
-                        P[t] = mfma16(wh, yl, P[t]);
-                        P[t] = mfma16(wl, yh, P[t]);
-                    }
-                }
-            }
-        }
-        f16v h0[HT], h1[HT];
-#pragma unroll
-        for (int t = 0; t < HT; ++t) {
-            h0[t] = zero;
-            h1[t] = zero;
-        }
-        float xb = 1.0f;
-        V fh[KB], fl[KB];
-        to_frags<HT, SPLIT>(h0, fh, fl);
-        for (int ii = 0; ii < N; ++ii) {
-            const int jj = a.rev ? N - 1 - ii : ii;
-            const float xbe = half ? xb : 1.0f;
-            // ================= layer 0: hidden tile 0 (r0, z0, n0), then tile 1 with tile 0's update beside it
-            f16v g0[3] = {P[0], P[HT], zero};
-#pragma unroll
-            for (int q = 0; q < KB; ++q) {
-                V ah[3], al[3];
-                load_frags<SPLIT, 3>(smem4, 0, T0, q, lane, ah, al);
-                mfma_frags<SPLIT, 3>(g0, ah, al, fh[q], fl[q]);
-            }
-#pragma unroll
-            for (int u = 0; u < 3; ++u) g0[u] = mfma(smem[G::OFF_X + T0[u] * 64 + lane], xbe, g0[u]);
-            const f16v ain0 = mfma(smem[G::OFF_IN + 0 * 64 + lane], xbe, P[2 * HT + 0]);
-            f16v g1[3] = {P[1], P[HT + 1], zero};
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < KB; ++q) {
-                V ah[3], al[3];
-                load_frags<SPLIT, 3>(smem4, 0, T1, q, lane, ah, al);
-                update_elems<SPLIT>(h0[0], g0[0], g0[1], ain0, g0[2], 4 * q, 4 * q + 4);
-                mfma_frags<SPLIT, 3>(g1, ah, al, fh[q], fl[q]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int u = 0; u < 3; ++u) g1[u] = mfma(smem[G::OFF_X + T1[u] * 64 + lane], xbe, g1[u]);
-            const f16v ain1 = mfma(smem[G::OFF_IN + 1 * 64 + lane], xbe, P[2 * HT + 1]);
-            // ================= layer 1, W_hh1 h1 part of hidden tile 0 (independent of h0'), beside tile 1's
-            // layer-0 update
-            V gh[KB], gl[KB];
-            to_frags<HT, SPLIT>(h1, gh, gl);
-            f16v k0[3] = {zero, zero, zero};  // r0, z0 (W_hh1 part, continued with W_ih1 below), hn0
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < KB; ++q) {
-                V ah[3], al[3];
-                load_frags<SPLIT, 3>(smem4, 2, T0, q, lane, ah, al);
-                update_elems<SPLIT>(h0[1], g1[0], g1[1], ain1, g1[2], 4 * q, 4 * q + 4);
-                mfma_frags<SPLIT, 3>(k0, ah, al, gh[q], gl[q]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            to_frags<HT, SPLIT>(h0, fh, fl);  // h0' for layer 1 and the next step's layer 0
-            // hidden tile 0: r0, z0 += W_ih1 h0' ; in0 = W_ih1_n h0'
-            f16v i0 = zero;
-            {
-                f16v t3[3] = {k0[0], k0[1], zero};
-#pragma unroll
-                for (int q = 0; q < KB; ++q) {
-                    V ah[3], al[3];
-                    load_frags<SPLIT, 3>(smem4, 1, T0, q, lane, ah, al);
-                    mfma_frags<SPLIT, 3>(t3, ah, al, fh[q], fl[q]);
-                }
-                k0[0] = t3[0];
-                k0[1] = t3[1];
-                i0 = t3[2];
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) k0[u] = mfma(smem[G::OFF_X + (TT + T0[u]) * 64 + lane], one_or_zero, k0[u]);
-            i0 = mfma(smem[G::OFF_X + (TT + T0[2]) * 64 + lane], one_or_zero, i0);
-            k0[2] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + 0) * 64 + lane], one_or_zero, k0[2]);
-            // hidden tile 1 (both layer-1 matrices) beside tile 0's layer-1 update
-            f16v k1[3] = {zero, zero, zero};
-            f16v i1 = zero;
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < KB; ++q) {
-                V ah[3], al[3], bh3[3], bl3[3];
-                load_frags<SPLIT, 3>(smem4, 2, T1, q, lane, ah, al);
-                load_frags<SPLIT, 3>(smem4, 1, T1, q, lane, bh3, bl3);
-                update_elems<SPLIT>(h1[0], k0[0], k0[1], i0, k0[2], 4 * q, 4 * q + 4);
-                mfma_frags<SPLIT, 3>(k1, ah, al, gh[q], gl[q]);
-                f16v t3[3] = {k1[0], k1[1], i1};
-                mfma_frags<SPLIT, 3>(t3, bh3, bl3, fh[q], fl[q]);
-                k1[0] = t3[0];
-                k1[1] = t3[1];
-                i1 = t3[2];
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) k1[u] = mfma(smem[G::OFF_X + (TT + T1[u]) * 64 + lane], one_or_zero, k1[u]);
-            i1 = mfma(smem[G::OFF_X + (TT + T1[2]) * 64 + lane], one_or_zero, i1);
-            k1[2] = mfma(smem[G::OFF_X + (2 * TT + 2 * HT + 1) * 64 + lane], one_or_zero, k1[2]);
-            update_elems<SPLIT>(h1[1], k1[0], k1[1], i1, k1[2], 0, 16);
-            float part = 0.0f;
-#pragma unroll
-            for (int t = 0; t < HT; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) part += smem[G::OFF_WL + (half * HT + t) * 16 + i] * h1[t][i];
-            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
-            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
-            float d;
-            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
-            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
-            if (half == 0 && valid) {
-                a.decoded[cw * N + jj] = d;
-                if (a.logits) a.logits[cw * N + ii] = out;
-            }
-            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
-            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
-        }
-    }
-}
-
 static uint16_t bf16_rne(float f) {
     uint32_t u;
     memcpy(&u, &f, 4);
@@ -1065,22 +792,10 @@ static void build_image_bf(const float* W, int N, int onehot, std::vector<float>
     wy_lo = (int64_t)(per / 8);  // in 16-B fragments
 }
 
-static bool gru_grouped() {  // NPD_GRU_GROUPED=0: the plain-order split kernel at F = 64, 2 layers (A/B)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_GRU_GROUPED");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
 template <int F, int L, int SPLIT>
 static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
     using G = GeoB<F, L, SPLIT>;
     auto kern = gru_decode_bf_kernel<F, L, SPLIT>;
-    if constexpr (F == 64 && L == 2) {
-        if (gru_grouped()) kern = gru_grouped_kernel<SPLIT>;
-    }
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -1090,11 +805,6 @@ static int launch_bf(const npd_gru* g, const ArgsB& a, hipStream_t s) {
     const int64_t tiles = (a.B + 31) / 32;
     const int64_t wgs = (tiles + NPD_GRU_BF_WPB - 1) / NPD_GRU_BF_WPB;
     const int grid = grid_for(wgs, 1, device_cu_count());
-    static bool attr2 = false;
-    if (!attr2) {
-        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
-        attr2 = true;
-    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU_BF_WPB), lds, s, a);
     (void)g;
     return launch_check("gru_decode_bf_kernel launch");
@@ -1135,19 +845,6 @@ __device__ __forceinline__ f4 mfma16s(const bf8& a, const bf8& b, const f4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int SPLIT>
-__device__ __forceinline__ void update4(f4& h, const f4& ar, const f4& az, const f4& ain, const f4& ahn) {
-    constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * ar[i]));
-        const float z = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c1 * az[i]));
-        const float x = ain[i] + ahn[i] * r;
-        const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(c2 * x)), -1.0f);
-        h[i] = (h[i] - nn) * z + nn;
-    }
-}
-
 // B fragments of a state: fragment kb, element j = tile 2kb + (j >> 2), register j & 3 (hi and, split, lo)
 template <int SPLIT>
 __device__ __forceinline__ void split16s(const f4 (&h)[4], typename SplitT<SPLIT>::V (&hi)[2],
@@ -1164,37 +861,10 @@ __device__ __forceinline__ void split16s(const f4 (&h)[4], typename SplitT<SPLIT
         }
 }
 
-// acc[u] += W_g[row tile t[u]] . state over both K blocks
 // LDS fragment of the 16-codeword image: wb = this lane's byte base of the matrix (laundered once per kernel)
 __device__ __forceinline__ f4 frag16(const f4* __restrict__ smem4, uint32_t wb, int t, int kb, int part) {
     return *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(smem4) + wb +
                                         ((t * Geo16::KB + kb) * 2 + part) * 1024);
-}
-
-template <int SPLIT, int NU>
-__device__ __forceinline__ void gemm16s(const f4* __restrict__ smem4, uint32_t wb, const int (&t)[NU],
-                                        f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
-                                        const typename SplitT<SPLIT>::V (&bl)[2]) {
-    using G = Geo16;
-    using V = typename SplitT<SPLIT>::V;
-#pragma unroll
-    for (int kb = 0; kb < G::KB; ++kb) {
-        V ah[NU], al[NU];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            ah[u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 0));
-            if (SplitT<SPLIT>::kLo) al[u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 1));
-        }
-        asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            acc[u] = mfma16s(ah[u], bh[kb], acc[u]);
-            if (SplitT<SPLIT>::kLo) {
-                acc[u] = mfma16s(ah[u], bl[kb], acc[u]);
-                acc[u] = mfma16s(al[u], bh[kb], acc[u]);
-            }
-        }
-    }
 }
 
 // (p_row0 + p_row1) + (p_row2 + p_row3) over the four 16-lane rows, the same in every lane (the order of
@@ -1211,133 +881,8 @@ __device__ __forceinline__ f4 fma4(float x, const f4& c, const f4& p) {
 }
 
 #define NPD_GRU16_WPB 8
-template <int SPLIT>
-__global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16_kernel(const ArgsB a) {
-    using G = Geo16;
-    using S = SplitT<SPLIT>;
-    using V = typename S::V;
-    using E = typename S::E;
-    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
-    const float* smem = reinterpret_cast<const float*>(smem4);
-    {
-        const f4* src = reinterpret_cast<const f4*>(a.img);
-        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int g4 = lane >> 4;
-    const int col = lane & 15;
-    const int N = a.N;
-    const int nkb = N / 32;
-    const int64_t ntiles = (a.B + 15) / 16;
-    // rows 4 g4 .. 4 g4 + 3 of 16-row tile t of a constant vector
-    // per-lane LDS byte bases, laundered so that every fragment / constant read is base + immediate offset
-    uint32_t wbs[3];
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-        uint32_t v = g * G::G_BYTES + lane * 16;
-        asm volatile("" : "+v"(v));
-        wbs[g] = v;
-    }
-    uint32_t cb = (G::OFF_C + 4 * g4) * 4;
-    asm volatile("" : "+v"(cb));
-    auto c4 = [&](int off, int t) -> f4 {
-        return *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(smem4) + cb + (off - G::OFF_C + 16 * t) * 4);
-    };
-    const f4 zero = {0.f, 0.f, 0.f, 0.f};
-
-    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU16_WPB + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * NPD_GRU16_WPB) {
-        const int64_t cw = tile * 16 + col;
-        const bool valid = cw < a.B;
-        const int64_t cwc = valid ? cw : a.B - 1;
-        // ---- P = consts + W_ih0[:, :N] . y ; K block kb covers y[32 kb + 8 g4 .. + 7]
-        f4 P[G::RT];
-#pragma unroll
-        for (int t = 0; t < G::RT; ++t) P[t] = c4(G::C0L0, t);
-        {
-            const float* yr = a.y + cwc * N;
-            for (int kb = 0; kb < nkb; ++kb) {
-                const f4 y0 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4);
-                const f4 y1 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4 + 4);
-                V yh, yl;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
-                    yh[j] = (E)v;
-                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
-                }
-#pragma unroll
-                for (int t = 0; t < G::RT; ++t) {
-                    const V wh = __builtin_bit_cast(V, a.wy[(t * nkb + kb) * 64 + lane]);
-                    P[t] = mfma16s(wh, yh, P[t]);
-                    if (S::kLo) {
-                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nkb + kb) * 64 + lane]);
-                        P[t] = mfma16s(wh, yl, P[t]);
-                        P[t] = mfma16s(wl, yh, P[t]);
-                    }
-                }
-            }
-        }
-        f4 h0[4], h1[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            h0[t] = zero;
-            h1[t] = zero;
-        }
-        V fh[2], fl[2];
-        split16s<SPLIT>(h0, fh, fl);
-        float xb = 1.0f;  // x_i column of the one-hot input (or the previous decision's sign)
-        for (int ii = 0; ii < N; ++ii) {
-            const int jj = a.rev ? N - 1 - ii : ii;
-            // ================= layer 0, hidden tile by hidden tile (r, z, hn rows of tile ht)
-#pragma unroll
-            for (int ht = 0; ht < 4; ++ht) {
-                const int T[3] = {ht, 4 + ht, 8 + ht};
-                f4 acc[3] = {fma4(xb, c4(G::C1L0, ht), P[ht]), fma4(xb, c4(G::C1L0, 4 + ht), P[4 + ht]),
-                             c4(G::BHN0, ht)};
-                gemm16s<SPLIT, 3>(smem4, wbs[0], T, acc, fh, fl);
-                const f4 ain = fma4(xb, c4(G::C1L0, 8 + ht), P[8 + ht]);
-                update4<SPLIT>(h0[ht], acc[0], acc[1], ain, acc[2]);
-            }
-            V gh[2], gl[2];
-            split16s<SPLIT>(h1, gh, gl);
-            split16s<SPLIT>(h0, fh, fl);  // h0' for layer 1 and the next step's layer 0
-            // ================= layer 1: r, z = c + W_ih1 h0' + W_hh1 h1 ; in = c + W_ih1_n h0' ; hn = c + W_hh1_n h1
-#pragma unroll
-            for (int ht = 0; ht < 4; ++ht) {
-                const int T[3] = {ht, 4 + ht, 8 + ht};
-                f4 ai[3] = {c4(G::C0L1, ht), c4(G::C0L1, 4 + ht), c4(G::C0L1, 8 + ht)};
-                gemm16s<SPLIT, 3>(smem4, wbs[1], T, ai, fh, fl);
-                f4 ah[3] = {ai[0], ai[1], c4(G::BHN1, ht)};
-                gemm16s<SPLIT, 3>(smem4, wbs[2], T, ah, gh, gl);
-                update4<SPLIT>(h1[ht], ah[0], ah[1], ai[2], ah[2]);
-            }
-            // ================= output: Linear(F, 1), reduced over the four lane groups
-            float part = 0.0f;
-#pragma unroll
-            for (int ht = 0; ht < 4; ++ht) {
-                const f4 wl = c4(G::WLIN, ht);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) part += wl[i] * h1[ht][i];
-            }
-            const float out = sum_rows16(part) + a.b_lin;
-            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
-            float d;
-            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
-            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
-            if (g4 == 0 && valid) {
-                a.decoded[cw * N + jj] = d;
-                if (a.logits) a.logits[cw * N + ii] = out;
-            }
-            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
-            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
-        }
-    }
-}
-
-// ---- software-pipelined variant (NPD_GRU16=2 A/B).  A wave's own VALU instructions issue in the gaps of its 16-bit
+// ---- the step is software-pipelined (measured 14.86 -> 14.42 ms per 2^20 words against the plain tile-by-tile
+// order, profiles/round3/gru_split_ab.txt; the plain order was removed in round 4).  A wave's own VALU instructions issue in the gaps of its 16-bit
 // MFMAs (8 of the 16 cycles of a 16x16x32 are busy for vector issue, MI355X_MICROARCH.md), while another wave's
 // do not (profiles/round3/coissue.txt: an fp16 MFMA wave and an FMA wave on one SIMD take the sum of their times).
 // So each hidden tile's GEMM carries the update of the PREVIOUS tile (cut into 12 chunks of ~5 instructions:
@@ -1416,7 +961,6 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
     using V = typename S::V;
     using E = typename S::E;
     extern __shared__ __attribute__((aligned(16))) f4 smem4[];
-    const float* smem = reinterpret_cast<const float*>(smem4);
     {
         const f4* src = reinterpret_cast<const f4*>(a.img);
         for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
@@ -1574,7 +1118,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
     }
 }
 
-// image of gru16_kernel: weight fragments (hi, lo) in the 16x16x32 A-operand order, constants x kc
+// image of gru16p_kernel: weight fragments (hi, lo) in the 16x16x32 A-operand order, constants x kc
 template <int SPLIT>
 static void build_image16(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
                           int64_t& wy_lo) {
@@ -1647,315 +1191,9 @@ static void build_image16(const float* W, int N, int onehot, std::vector<float>&
     wy_lo = (int64_t)(per / 8);
 }
 
-// ---- 32-codeword pipelined variant (NPD_GRU16=3 A/B): the same pipeline on v_mfma_f32_32x32x16 at ONE wave per SIMD.
-// PMC of gru16_kernel (profiles/round3/pmc_gru16_summary.json): MFMA busy 0.46 and VALU active 0.57 of the SIMD's
-// cycles -- the two serialise.  A 32x32x16 MFMA leaves 24 of its 32 cycles free for the same wave's VALU issue
-// (a 16x16x32 leaves 8 of 16), so the update chunks of the previous tile fit beside the current tile's MFMAs.
-// Weights and the y projection use the 32-codeword split image (GeoB, build_image_bf); constants follow in the
-// 32x32 accumulator order: vector V, tile t (32 rows), lane half h, register i = row (i&3) + 8(i>>2) + 4h.
-struct Geo32 {
-    static constexpr int TT = 6, HT = 2, KB = 4;
-    static constexpr int IMG4 = 3 * TT * KB * 64;  // 16-B fragments per split image (= GeoB<64, 2, *>::IMG / 4)
-    static constexpr int OFF_C = 2 * IMG4 * 4;
-    static constexpr int C0L0 = OFF_C, C1L0 = OFF_C + 192, BHN0 = OFF_C + 384, C0L1 = OFF_C + 448,
-                         BHN1 = OFF_C + 640, WLIN = OFF_C + 704, TOTAL = OFF_C + 768;
-};
-
-template <int SPLIT>
-struct Upd16 {
-    f16v er, ez, en, z;
-    template <int C>
-    __device__ __forceinline__ void step(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
-        constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
-        constexpr int i = C / 3, st = C % 3;
-        if constexpr (st == 0) {
-            er[i] = __builtin_amdgcn_exp2f(c1 * ar[i]);
-            ez[i] = __builtin_amdgcn_exp2f(c1 * az[i]);
-        } else if constexpr (st == 1) {
-            const float r = __builtin_amdgcn_rcpf(1.0f + er[i]);
-            z[i] = __builtin_amdgcn_rcpf(1.0f + ez[i]);
-            en[i] = __builtin_amdgcn_exp2f(c2 * (ain[i] + ahn[i] * r));
-        } else {
-            const float nn = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + en[i]), -1.0f);
-            h[i] = (h[i] - nn) * z[i] + nn;
-        }
-    }
-};
-
-// B fragment q = 2t + s of a state: registers 8s .. 8s + 7 of tile t
-template <int SPLIT>
-__device__ __forceinline__ void split_q(const f16v (&h)[2], int q, typename SplitT<SPLIT>::V (&hi)[4],
-                                        typename SplitT<SPLIT>::V (&lo)[4]) {
-    using S = SplitT<SPLIT>;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float v = h[q >> 1][8 * (q & 1) + j] * S::kIn;
-        const typename S::E b = (typename S::E)v;
-        hi[q][j] = b;
-        if (S::kLo) lo[q][j] = (typename S::E)(v - (float)b);
-    }
-}
-
-__device__ __forceinline__ f16v fma16v(float x, const f16v& c, const f16v& p) {
-    f16v r;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) r[i] = fmaf(x, c[i], p[i]);
-    return r;
-}
-
-// acc[u] += W_g[32-row tile t[u]] . state over the 4 K steps (fragments of step q+1 loaded beside step q's MFMAs);
-// work chunks C0 .. C0 + NCH - 1 spread over the 4 NU MFMA triples, one sched_barrier-fenced region per triple
-template <int SPLIT, int NU, int C0, int NCH, typename Work>
-__device__ __forceinline__ void gemm32i(const f4* __restrict__ smem4, int g, const int (&t)[NU], int lane,
-                                        f16v (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[4],
-                                        const typename SplitT<SPLIT>::V (&bl)[4], Work&& work) {
-    using G = Geo32;
-    using V = typename SplitT<SPLIT>::V;
-    constexpr int NT = 4 * NU;
-    V ah[2][NU], al[2][NU];
-    auto load = [&](int q, int b) {
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int idx = ((g * G::TT + t[u]) * G::KB + q) * 64 + lane;
-            ah[b][u] = __builtin_bit_cast(V, smem4[idx]);
-            if (SplitT<SPLIT>::kLo) al[b][u] = __builtin_bit_cast(V, smem4[G::IMG4 + idx]);
-        }
-    };
-    load(0, 0);
-    static_for<0, 4>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        if constexpr (q + 1 < 4) load(q + 1, (q + 1) & 1);
-        asm volatile("" ::: "memory");  // loop-invariant LDS reads stay in the step loop, one K step ahead
-        static_for<0, NU>([&](auto uc) {
-            constexpr int u = decltype(uc)::value;
-            constexpr int tr = q * NU + u;
-            acc[u] = mfma16(ah[q & 1][u], bh[q], acc[u]);
-            if (SplitT<SPLIT>::kLo) {
-                acc[u] = mfma16(ah[q & 1][u], bl[q], acc[u]);
-                acc[u] = mfma16(al[q & 1][u], bh[q], acc[u]);
-            }
-            static_for<C0 + NCH * tr / NT, C0 + NCH * (tr + 1) / NT>([&](auto cc) { work(cc); });
-            __builtin_amdgcn_sched_barrier(0);
-        });
-    });
-}
-
-#define NPD_GRU32_WPB 4
-template <int SPLIT>
-__global__ __launch_bounds__(64 * NPD_GRU32_WPB) void gru32p_kernel(const ArgsB a) {
-    using G = Geo32;
-    using S = SplitT<SPLIT>;
-    using V = typename S::V;
-    using E = typename S::E;
-    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
-    const float* smem = reinterpret_cast<const float*>(smem4);
-    {
-        const f4* src = reinterpret_cast<const f4*>(a.img);
-        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int half = lane >> 5;
-    const int col = lane & 31;
-    const int N = a.N;
-    const int64_t ntiles = (a.B + 31) / 32;
-    // this lane's 16 accumulator-row values of 32-row tile t of a constant vector
-    auto c16 = [&](int off, int t) -> f16v {
-        const f4* p = reinterpret_cast<const f4*>(smem + off + (2 * t + half) * 16);
-        const f4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
-        return f16v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
-                    x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
-    };
-    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    constexpr int T0[3] = {0, 2, 4};  // hidden tile 0: r, z, n rows
-    constexpr int T1[3] = {1, 3, 5};
-    auto nowork = [](auto) {};
-
-    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU32_WPB + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * NPD_GRU32_WPB) {
-        const int64_t cw = tile * 32 + col;
-        const bool valid = cw < a.B;
-        const int64_t cwc = valid ? cw : a.B - 1;
-        f16v P[G::TT];
-#pragma unroll
-        for (int t = 0; t < G::TT; ++t) P[t] = c16(G::C0L0, t);
-        {
-            const float* yr = a.y + cwc * N;
-            const int nq = N / 16;
-            for (int q = 0; q < nq; ++q) {
-                const f4 y0 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half);
-                const f4 y1 = *reinterpret_cast<const f4*>(yr + 16 * q + 8 * half + 4);
-                V yh, yl;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float v = (j < 4 ? y0[j] : y1[j - 4]) * S::kIn;
-                    yh[j] = (E)v;
-                    if (S::kLo) yl[j] = (E)(v - (float)yh[j]);
-                }
-#pragma unroll
-                for (int t = 0; t < G::TT; ++t) {
-                    const V wh = __builtin_bit_cast(V, a.wy[(t * nq + q) * 64 + lane]);
-                    P[t] = mfma16(wh, yh, P[t]);
-                    if (S::kLo) {
-                        const V wl = __builtin_bit_cast(V, a.wy[a.wy_lo + (t * nq + q) * 64 + lane]);
-                        P[t] = mfma16(wh, yl, P[t]);
-                        P[t] = mfma16(wl, yh, P[t]);
-                    }
-                }
-            }
-        }
-        f16v h0[2] = {zero, zero}, h1[2] = {zero, zero};
-        V fh[4], fl[4], gh[4], gl[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            split_q<SPLIT>(h0, q, fh, fl);
-            split_q<SPLIT>(h1, q, gh, gl);
-        }
-        float xb = 1.0f;
-        // P enters the r / z accumulators as the first MFMA's C operand (no VALU read of P); the x_i column is
-        // added after the GEMM
-        f16v a0[3] = {P[0], P[2], c16(G::BHN0, 0)};
-        gemm32i<SPLIT, 3, 0, 0>(smem4, 0, T0, lane, a0, fh, fl, nowork);
-        for (int ii = 0; ii < N; ++ii) {
-            const int jj = a.rev ? N - 1 - ii : ii;
-            Upd16<SPLIT> u;
-            // ================= layer 0: finish hidden tile 0, then tile 1 beside tile 0's update
-            const f16v ap0 = fma16v(xb, c16(G::C1L0, 0), a0[0]);
-            const f16v ap1 = fma16v(xb, c16(G::C1L0, 2), a0[1]);
-            const f16v ap2 = a0[2];
-            const f16v ain0 = fma16v(xb, c16(G::C1L0, 4), P[4]);
-            f16v acc[3] = {P[1], P[3], c16(G::BHN0, 1)};
-            gemm32i<SPLIT, 3, 0, 48>(smem4, 0, T1, lane, acc, fh, fl, [&](auto cc) {
-                u.template step<decltype(cc)::value>(h0[0], ap0, ap1, ain0, ap2);
-            });
-            acc[0] = fma16v(xb, c16(G::C1L0, 1), acc[0]);
-            acc[1] = fma16v(xb, c16(G::C1L0, 3), acc[1]);
-            const f16v ain1 = fma16v(xb, c16(G::C1L0, 5), P[5]);
-            // ================= layer 1, tile 0: W_hh1 h1 beside h0 tile 1's update and the h0' split
-            f16v b[3] = {c16(G::C0L1, 0), c16(G::C0L1, 2), c16(G::BHN1, 0)};
-            gemm32i<SPLIT, 3, 0, 52>(smem4, 2, T0, lane, b, gh, gl, [&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                if constexpr (c < 48) u.template step<c>(h0[1], acc[0], acc[1], ain1, acc[2]);
-                else split_q<SPLIT>(h0, c - 48, fh, fl);
-            });
-            f16v bi[3] = {b[0], b[1], c16(G::C0L1, 4)};
-            gemm32i<SPLIT, 3, 0, 0>(smem4, 1, T0, lane, bi, fh, fl, nowork);
-            // ================= layer 1, tile 1 beside h1 tile 0's update and its output partial sum
-            float part = 0.0f;
-            auto work1 = [&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                if constexpr (c < 48) {
-                    u.template step<c>(h1[0], bi[0], bi[1], bi[2], b[2]);
-                } else {
-                    const f16v wl = c16(G::WLIN, 0);
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) part = fmaf(wl[i], h1[0][i], part);
-                }
-            };
-            f16v bb[3] = {c16(G::C0L1, 1), c16(G::C0L1, 3), c16(G::BHN1, 1)};
-            gemm32i<SPLIT, 3, 0, 25>(smem4, 2, T1, lane, bb, gh, gl, work1);
-            f16v bbi[3] = {bb[0], bb[1], c16(G::C0L1, 5)};
-            gemm32i<SPLIT, 3, 25, 24>(smem4, 1, T1, lane, bbi, fh, fl, work1);
-            // ================= tail: next step's layer-0 tile-0 GEMM beside h1 tile 1's update, the output, the
-            // decision and the h1 split
-            a0[0] = P[0];
-            a0[1] = P[2];
-            a0[2] = c16(G::BHN0, 0);
-            gemm32i<SPLIT, 3, 0, 53>(smem4, 0, T0, lane, a0, fh, fl, [&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                if constexpr (c < 48) {
-                    u.template step<c>(h1[1], bbi[0], bbi[1], bbi[2], bb[2]);
-                } else if constexpr (c == 48) {
-                    const f16v wl = c16(G::WLIN, 1);
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) part = fmaf(wl[i], h1[1][i], part);
-                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
-                    const float out = (__uint_as_float(r[0]) + __uint_as_float(r[1])) + a.b_lin;
-                    const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
-                    float d;
-                    if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
-                    else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
-                    if (half == 0 && valid) {
-                        a.decoded[cw * N + jj] = d;
-                        if (a.logits) a.logits[cw * N + ii] = out;
-                    }
-                    const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
-                    xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
-                } else {
-                    split_q<SPLIT>(h1, c - 49, gh, gl);
-                }
-            });
-        }
-    }
-}
-
-// image of gru32p_kernel: the 32-codeword split weight images (build_image_bf) + constants in 32x32 row order
-template <int SPLIT>
-static void build_image32(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
-                          int64_t& wy_lo) {
-    using G = Geo32;
-    std::vector<float> imgB, img16, wy16;
-    float b_lin = 0.0f;
-    build_image_bf<64, 2, SPLIT>(W, N, onehot, imgB, wy, b_lin, wy_lo);
-    int64_t dummy = 0;
-    build_image16<SPLIT>(W, N, onehot, img16, wy16, dummy);  // its constants (row-major) are reused
-    img.assign(G::TOTAL, 0.0f);
-    const int nw = (int)imgB.size() < G::OFF_C ? (int)imgB.size() : G::OFF_C;  // plain bf16: no lo image
-    for (int i = 0; i < nw; ++i) img[i] = imgB[i];
-    const int vec[6][2] = {{G::C0L0, Geo16::C0L0}, {G::C1L0, Geo16::C1L0}, {G::BHN0, Geo16::BHN0},
-                           {G::C0L1, Geo16::C0L1}, {G::BHN1, Geo16::BHN1}, {G::WLIN, Geo16::WLIN}};
-    const int rows[6] = {192, 192, 64, 192, 64, 64};
-    for (int v = 0; v < 6; ++v)
-        for (int t = 0; t < rows[v] / 32; ++t)
-            for (int h = 0; h < 2; ++h)
-                for (int i = 0; i < 16; ++i)
-                    img[vec[v][0] + (2 * t + h) * 16 + i] = img16[vec[v][1] + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h];
-}
-
-// NPD_GRU16=0: the 32-codeword split kernels; 1: gru16_kernel; 2 (default, measured best): gru16p_kernel;
-// 3: gru32p_kernel (A/B)
-static int gru16_mode() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_GRU16");
-        v = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
-    }
-    return v;
-}
-static bool gru16_enabled() { return gru16_mode() != 0; }
-
-template <int SPLIT>
-static int launch32p(const ArgsB& a, hipStream_t s) {
-    auto kern = gru32p_kernel<SPLIT>;
-    static bool attr = false;
-    if (!attr) {
-        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
-        attr = true;
-    }
-    const int64_t tiles = (a.B + 31) / 32;
-    const int64_t wgs = (tiles + NPD_GRU32_WPB - 1) / NPD_GRU32_WPB;
-    const int grid = grid_for(wgs, 1, device_cu_count());
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU32_WPB), (size_t)Geo32::TOTAL * 4, s, a);
-    return launch_check("gru32p_kernel launch");
-}
-
-// NPD_GRU_FOLD=0: the scaled fp16 split (SPLIT 4) instead of the folded one (SPLIT 5) in the 16-codeword kernels
-static bool gru_fold() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_GRU_FOLD");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
 template <int SPLIT>
 static int launch16(const ArgsB& a, hipStream_t s) {
-    if constexpr (SPLIT != 5) {
-        if (gru16_mode() == 3) return launch32p<SPLIT>(a, s);
-    }
-    auto kern = gru16_mode() == 2 ? gru16p_kernel<SPLIT> : gru16_kernel<SPLIT>;
+    auto kern = gru16p_kernel<SPLIT>;
     static bool attr = false;
     if (!attr) {
         NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
@@ -1965,7 +1203,7 @@ static int launch16(const ArgsB& a, hipStream_t s) {
     const int64_t wgs = (tiles + NPD_GRU16_WPB - 1) / NPD_GRU16_WPB;
     const int grid = grid_for(wgs, 1, device_cu_count());
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU16_WPB), (size_t)Geo16::TOTAL * 4, s, a);
-    return launch_check("gru16_kernel launch");
+    return launch_check("gru16p_kernel launch");
 }
 
 // =============================================================================== wide hidden sizes
@@ -2199,7 +1437,7 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
             "npd_gru_create: F = 512 with 2 layers needs N <= 128 (LDS holds both states and the tile's y)");
     NPD_ARG(layers == 1 || layers == 2, "npd_gru_create: 1 or 2 GRU layers supported");
     NPD_ARG(precision >= 0 && precision <= 3,
-            "npd_gru_create: precision must be 0 (fp32), 1 (bf16x3), 2 (bf16) or 3 (fp16x3, scaled)");
+            "npd_gru_create: precision must be 0 (fp32), 1 (bf16x3), 2 (bf16) or 3 (fp16x3)");
     NPD_ARG(precision == 0 || N % 16 == 0, "npd_gru_create: bf16 paths need N % 16 == 0");
     const int Din = N + (onehot ? 2 : 1);
     int64_t expect = (int64_t)3 * F * Din + (int64_t)3 * F * F + 6 * F;
@@ -2211,7 +1449,7 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     int64_t wy_lo = 0;
 #define NPD_BUILD(FF, LL)                                                                              \
     do {                                                                                               \
-        if (precision == 0) gru::build_image<FF, LL>(weights, N, onehot, img, wy, b_lin, gru::gru_fold32()); \
+        if (precision == 0) gru::build_image<FF, LL>(weights, N, onehot, img, wy, b_lin, true);           \
         else if (precision == 1) gru::build_image_bf<FF, LL, 3>(weights, N, onehot, img, wy, b_lin, wy_lo); \
         else if (precision == 3) gru::build_image_bf<FF, LL, 4>(weights, N, onehot, img, wy, b_lin, wy_lo); \
         else gru::build_image_bf<FF, LL, 1>(weights, N, onehot, img, wy, b_lin, wy_lo);               \
@@ -2231,19 +1469,15 @@ extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float*
     if (!g) return fail(NPD_ENOMEM, "npd_gru_create: out of memory");
     memset(g, 0, sizeof(*g));
     g->N = N; g->F = F; g->layers = layers; g->onehot = onehot; g->precision = precision; g->b_lin = b_lin;
-    g->fold32 = precision == 0 && F <= 64 && gru::gru_fold32();
     g->img_floats = (int64_t)img.size();
     g->wy_lo = wy_lo;
     std::vector<float> img16, wy16;
     if (precision != 0 && F == 64 && layers == 2 && N % 32 == 0) {
-        g->split16 = precision == 1 ? 3 : precision == 3 ? (gru::gru16_mode() != 3 && gru::gru_fold() ? 5 : 4) : 1;
-        if (gru::gru16_mode() == 3) {
-            if (precision == 1) gru::build_image32<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
-            else if (precision == 3) gru::build_image32<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
-            else gru::build_image32<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
-        } else if (precision == 1) gru::build_image16<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
-        else if (g->split16 == 5) gru::build_image16<5>(weights, N, onehot, img16, wy16, g->wy16_lo);
-        else if (precision == 3) gru::build_image16<4>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        // fp16x3 here is the unscaled split with the gate constants folded into the weights (SPLIT 5); the
+        // 32-codeword kernels (other shapes) run the x 2^8-scaled split (SPLIT 4)
+        g->split16 = precision == 1 ? 3 : precision == 3 ? 5 : 1;
+        if (precision == 1) gru::build_image16<3>(weights, N, onehot, img16, wy16, g->wy16_lo);
+        else if (precision == 3) gru::build_image16<5>(weights, N, onehot, img16, wy16, g->wy16_lo);
         else gru::build_image16<1>(weights, N, onehot, img16, wy16, g->wy16_lo);
     }
     hipError_t e = hipGetDevice(&g->device);
@@ -2309,14 +1543,12 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
         b.y = y; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
         b.rev = a.rev; b.onehot = a.onehot; b.b_lin = g->b_lin; b.wy_lo = g->wy_lo;
         for (int w = 0; w < kMaxWords; ++w) b.info[w] = a.info[w];
-        if (g->img16 && gru::gru16_enabled()) {
+        if (g->img16) {
             b.img = g->img16;
             b.wy = reinterpret_cast<const gru::f4*>(g->wy16);
             b.wy_lo = g->wy16_lo;
-            return g->split16 == 3   ? gru::launch16<3>(b, s)
-                   : g->split16 == 5 ? gru::launch16<5>(b, s)
-                   : g->split16 == 4 ? gru::launch16<4>(b, s)
-                                     : gru::launch16<1>(b, s);
+            return g->split16 == 3 ? gru::launch16<3>(b, s) : g->split16 == 5 ? gru::launch16<5>(b, s)
+                                   : gru::launch16<1>(b, s);
         }
 #define NPD_LBF(FF, LL)                                                                                   \
         return g->precision == 1   ? gru::launch_bf<FF, LL, 3>(g, b, s)                                     \
@@ -2333,8 +1565,8 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
         if (g->F == 256) return g->layers == 2 ? gru::launch_wide<256, 2>(a, g->N, s) : gru::launch_wide<256, 1>(a, g->N, s);
         return g->layers == 2 ? gru::launch_wide<128, 2>(a, g->N, s) : gru::launch_wide<128, 1>(a, g->N, s);
     }
-    if (g->F == 64 && g->layers == 2) return gru::launch<64, 2>(g, a, s);
-    if (g->F == 64) return gru::launch<64, 1>(g, a, s);
-    if (g->layers == 2) return gru::launch<32, 2>(g, a, s);
-    return gru::launch<32, 1>(g, a, s);
+    if (g->F == 64 && g->layers == 2) return gru::launch<64, 2>(a, s);
+    if (g->F == 64) return gru::launch<64, 1>(a, s);
+    if (g->layers == 2) return gru::launch<32, 2>(a, s);
+    return gru::launch<32, 1>(a, s);
 }

@@ -513,8 +513,10 @@ __device__ __forceinline__ void dma_chunk(char* lds, uint32_t base, const Args& 
     const uint32_t v1 = (uint32_t)(((lane >> 3) * N + col0 + ((c0 ^ 4) << 2)) * 4);
 #pragma unroll
     for (int k = 0; k < 8; ++k)
+        // the row offset goes in voffset, not soffset: the descriptor's range check covers voffset + the
+        // immediate only, so rows past B must be addressed through voffset to read as zeros
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + base + k * 1024), 16,
-                                                 (k & 1) ? v1 : v0, 8 * k * N * 4, 0, 0);
+                                                 ((k & 1) ? v1 : v0) + (uint32_t)(8 * k * N * 4), 0, 0, 0);
 }
 
 // this lane's 32 values of the slot at `base` (waits for every outstanding DMA)
@@ -584,7 +586,7 @@ __device__ __forceinline__ void stage_tile_buf(char* lds, const Args& a, int64_t
     for (int k = 0; k < 32; ++k) {
         const uint32_t vo = (uint32_t)((hi * N + 4 * ((lane & 31) ^ (2 * (k & 7) + hi))) * 4);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + a.off_stage + k * 1024), 16,
-                                                 vo, 2 * k * N * 4, 0, 0);
+                                                 vo + (uint32_t)(2 * k * N * 4), 0, 0, 0);  // range-checked (dma_chunk)
     }
 }
 
@@ -1188,13 +1190,9 @@ int sc_fast_run(const CodeParams& p, const float* y, const float* llr_scale, int
                 unsigned long long* counters, uint64_t seed, uint64_t cw_offset, int64_t B, hipStream_t s);
 }  // namespace npd
 
-static bool fast_disabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("NPD_SC_GENERIC");  // force the generic kernel (testing / A-B)
-        v = (e && *e && *e != '0') ? 1 : 0;
-    }
-    return v == 1;
+static bool fast_disabled() {  // NPD_SC_GENERIC=1: force the generic kernel (testing / A-B); read per call
+    const char* e = getenv("NPD_SC_GENERIC");
+    return e && *e && *e != '0';
 }
 
 extern "C" int npd_sc_decode(const npd_code* code, const float* y, float llr_scale, float* leaf_llr, float* msg_hat,

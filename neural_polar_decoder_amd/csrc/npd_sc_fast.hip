@@ -654,20 +654,16 @@ static int launch(const CodeParams& p, Args a, hipStream_t s) {
 // measured 0.408 -> 0.398 ms per 5 x 2^20 (membench, same geometry: 5.24 -> 5.57 TB/s); the VALU-bound
 // fused Monte-Carlo kernel is 1 % faster with a workgroup's waves on adjacent tiles.  NPD_SCF_ILV=0/1
 // overrides both (A/B).
+// The switches are read per call (a getenv per launch), so a test can run both sides in one process.
 static uint32_t tile_interleave(bool gen) {
-    static const int v = [] {
-        const char* e = getenv("NPD_SCF_ILV");
-        return (e && *e) ? (e[0] == '1' ? 1 : 0) : -1;
-    }();
+    const char* e = getenv("NPD_SCF_ILV");
+    const int v = (e && *e) ? (e[0] == '1' ? 1 : 0) : -1;
     return v >= 0 ? (uint32_t)v : (gen ? 0u : 1u);
 }
 
 static bool spec_disabled() {
-    static const bool off = [] {
-        const char* e = getenv("NPD_SC_NOSPEC");
-        return e && e[0] == '1';
-    }();
-    return off;
+    const char* e = getenv("NPD_SC_NOSPEC");
+    return e && e[0] == '1';
 }
 
 // eligible: Polar, 8 <= N <= 64, K <= 128 (one Philox block of message bits), y 16-B aligned

@@ -98,8 +98,10 @@ class RNN_decoder:
     'y_input' runs fused on the GPU.
 
     ``precision`` (keyword, not in the reference): "fp32" (default; the reference's arithmetic),
-    "fp16x3" (scaled hi + lo fp16 split on the fp16 MFMA: three products per multiply, fp32 accumulation;
-    held to the fp32 path's tolerance, tests/test_gru_gpu.py), "bf16x3" (split-bf16, ~2^-16 relative per
+    "fp16x3" (hi + lo fp16 split on the fp16 MFMA: three products per multiply, fp32 accumulation; F = 64 with 2
+    layers and N % 32 == 0 runs the unscaled split, whose lo parts of weights / states below 2^-14 are fp16
+    subnormals (absolute resolution 2^-24); other shapes scale operands by 2^8 first; held to the fp32 path's
+    tolerance, tests/test_gru_gpu.py), "bf16x3" (split-bf16, ~2^-16 relative per
     product) or "bf16" (plain bf16 MFMA, fp32 accumulation).  The split paths cover hidden sizes <= 64."""
 
     PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16": 2, "fp16x3": 3}

@@ -1,0 +1,36 @@
+"""Trained CRISP fixture cases: code, GRU and curriculum (shared by gen_trained.py and train_crisp_gpu.py).
+
+Curricula follow run_crisp.sh:2-16: rate profile 'rev_polar' (Polar) / 'rev_RM' (PAC) with --target_K the
+final K, K + 1 per stage, --dec_train_snr 0, batch 4096, AdamW lr 1e-3, StepLR(2000, 0.95), teacher forcing
+ratio 1, a long final stage.  Each stage is (K, steps, trainer): trainer "ref" = the reference's own
+rnn_all.py, unmodified, on the CPU (gen_trained.py); "gpu" = train_crisp_gpu.py's restatement of the same
+loop on one MI355X.  GPU stages come first; the final stage(s) always run the reference's own loop.
+"""
+
+
+def _cur(first_K, first_steps, target_K, per_stage, final_gpu, final_ref, who="gpu"):
+    cur = [(first_K, first_steps, who)]
+    cur += [(k, per_stage, who) for k in range(first_K + 1, target_K)]
+    if final_gpu:
+        cur.append((target_K, final_gpu, who))
+    cur.append((target_K, final_ref, "ref"))
+    return cur
+
+
+_COMMON = dict(F=64, layers=2, snr_train=0.0, batch=4096, lr=1e-3, lr_decay=2000, lr_gamma=0.95,
+               eval_snrs=[0.0, 2.0, 4.0], n_dec=4096, n_mc=1 << 20)
+
+CASES = {
+    # entirely the reference's own loop (CPU): K = 4 .. 16
+    "trained_crisp_32_16": dict(_COMMON, code="Polar", profile="rev_polar", N=32, K=16, seed_init=3216,
+                                curriculum=_cur(4, 2000, 16, 1000, 0, 8000, who="ref"), ref_lr=1e-3,
+                                n_logit=512, n_sc=1 << 17, seed_dec=31, seed_mc=37),
+    # K = 8 .. 32 on the GPU, then the reference's loop at K = 32
+    "trained_crisp_64_32": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6432,
+                                curriculum=_cur(8, 5000, 32, 2000, 30000, 1000), ref_lr=2e-4,
+                                n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
+    # PAC(128,64) 'RM' (configs[3], rnn_all.py:61 --code PAC): K = 8 .. 64 on the GPU, then the reference's loop
+    "trained_pac_128_64": dict(_COMMON, code="PAC", profile="rev_RM", N=128, K=64, seed_init=12864,
+                               curriculum=_cur(8, 5000, 64, 1500, 30000, 400), ref_lr=2e-4,
+                               n_logit=256, n_sc=1 << 13, seed_dec=47, seed_mc=53),
+}

@@ -46,50 +46,52 @@ import torch  # noqa: E402
 
 SNRS = [0.0, 1.0, 2.0, 3.0, 4.0]
 
-# name -> code, GRU and curriculum [(K, steps), ...] (run_crisp.sh style: K grows to the target)
-CASES = {
-    "trained_crisp_32_16": dict(N=32, K=16, F=64, layers=2, snr_train=1.0, batch=4096, lr=1e-3,
-                                curriculum=[(4, 400), (8, 400), (12, 600), (16, 3000), (16, 6000)],
-                                n_dec=4096, n_logit=512, n_mc=1 << 20, n_sc=1 << 17, seed_dec=31, seed_mc=37),
-    "trained_crisp_64_32": dict(N=64, K=32, F=64, layers=2, snr_train=1.0, batch=4096, lr=1e-3,
-                                curriculum=[(8, 500), (12, 500), (16, 600), (20, 600), (24, 800), (28, 1000),
-                                            (32, 3000)],
-                                n_dec=4096, n_logit=256, n_mc=1 << 20, n_sc=1 << 16, seed_dec=41, seed_mc=43),
-}
+sys.path.insert(0, OUT)
+from crisp_cases import CASES  # noqa: E402
+
+TRAIN_STATE = os.path.join(os.path.dirname(os.path.dirname(OUT)), "train_state")
 
 
 def y_digest(y: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(y, np.float32).tobytes()).hexdigest()
 
 
-def train(name, c, workdir):
-    """Run the reference's training script over the curriculum; returns the final checkpoint path."""
+def train(name, c, workdir, gpu_weights=None):
+    """Run the reference's training script over the curriculum's "ref" stages; returns the final checkpoint
+    path.  A curriculum that starts with "gpu" stages continues from their weights (train_crisp_gpu.py's
+    --out file, default train_state/<name>.net.pt)."""
     wd = os.path.join(workdir, name)
     os.makedirs(wd, exist_ok=True)
     prev = None
+    if any(who == "gpu" for _, _, who in c["curriculum"]):
+        prev = gpu_weights or os.path.join(TRAIN_STATE, f"{name}.net.pt")
+        if not os.path.exists(prev):
+            raise SystemExit(f"{name}: GPU curriculum stages not run yet ({prev} missing; tests/golden/train_crisp_gpu.py)")
     seen = {}
-    for K, steps in c["curriculum"]:
+    path = None
+    for K, steps, who in c["curriculum"]:
+        if who != "ref":
+            continue
         seen[K] = seen.get(K, 0) + 1  # a K repeated in the curriculum continues from the previous stage
         path = os.path.join(wd, f"K{K}.pt" if seen[K] == 1 else f"K{K}_{seen[K]}.pt")
         if os.path.exists(path) and os.path.exists(path + ".done"):
-            if not os.path.exists(path + ".net"):
-                with torch.serialization.safe_globals([argparse.Namespace]):
-                    torch.save({"net": torch.load(path, map_location="cpu", weights_only=True)["net"]}, path + ".net")
             prev = path + ".net"
             continue
-        cmd = [sys.executable, "-u", os.path.join(REF, "rnn_all.py"), "--code", "Polar", "--rate_profile", "polar",
-               "--N", str(c["N"]), "--K", str(K), "--target_K", str(c["K"]), "--decoding_type", "y_input", "--onehot",
-               "--rnn_type", "GRU", "--rnn_feature_size", str(c["F"]), "--rnn_depth", str(c["layers"]),
-               "--num_steps", str(steps), "--batch_size", str(c["batch"]), "--tfr_min", "1", "--tfr_max", "1",
-               "--dec_train_snr", str(c["snr_train"]), "--lr", str(c["lr"]), "--scheduler", "step",
-               "--lr_decay", "2000", "--lr_decay_gamma", "0.95", "--print_freq", "200",
-               "--test_batch_size", "2000", "--test_size", "2000", "--model_save_per", "100000",
+        cmd = [sys.executable, "-u", os.path.join(REF, "rnn_all.py"), "--code", c["code"],
+               "--rate_profile", c["profile"], "--N", str(c["N"]), "--K", str(K), "--target_K", str(c["K"]),
+               "--decoding_type", "y_input", "--onehot", "--rnn_type", "GRU", "--rnn_feature_size", str(c["F"]),
+               "--rnn_depth", str(c["layers"]), "--num_steps", str(steps), "--batch_size", str(c["batch"]),
+               "--tfr_min", "1", "--tfr_max", "1", "--dec_train_snr", str(c["snr_train"]), "--lr", str(c["ref_lr"]),
+               "--scheduler", "step", "--lr_decay", str(c["lr_decay"]), "--lr_decay_gamma", str(c["lr_gamma"]),
+               "--print_freq", "250", "--test_batch_size", "2000", "--test_size", "2000", "--model_save_per", "100000",
                "--save_path", path, "--fresh"]
+        if c["code"] == "PAC":
+            cmd += ["--g", "91"]
         if prev:
             cmd += ["--load_path", prev]
         print("train:", name, f"K={K}", f"{steps} steps", flush=True)
         t0 = time.time()
-        log = os.path.join(wd, f"K{K}.log")
+        log = os.path.join(wd, f"K{K}_{seen[K]}.log")
         with open(log, "w") as f:
             subprocess.run(cmd, cwd=wd, stdout=f, stderr=subprocess.STDOUT,
                            env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))
@@ -123,8 +125,13 @@ def evaluate(name, c, ckpt):
     N, K, F = c["N"], c["K"], c["F"]
     rnn_m.args = argparse.Namespace(hard_decision=False, target_K=K, random_seed=42, loss_only=None, K=K, N=N,
                                     no_detach=False)
-    code = rnn_m.get_code("Polar", "polar", N, K)
-    info = np.asarray(code.info_positions, np.int64)
+    # the final code of the curriculum: the standard one ('polar' / 'RM' at K = target_K; rev_polar / rev_RM
+    # at K = target_K give the same sets)
+    if c["code"] == "Polar":
+        code = rnn_m.get_code("Polar", "polar", N, K)
+    else:
+        code = rnn_m.get_code("PAC", "RM", N, K, 91)
+    info = np.asarray(code.info_inds, np.int64)
     with torch.serialization.safe_globals([argparse.Namespace]):
         ck = torch.load(ckpt, map_location="cpu", weights_only=True)
     net = rnn_m.RNN_Model("GRU", N + 2, F, 1, c["layers"], N, 0, 0, "selu", 0.0, False, out_linear_depth=1)
@@ -136,7 +143,10 @@ def evaluate(name, c, ckpt):
 
     out = {"info": info, "N": np.int64(N), "K": np.int64(K), "F": np.int64(F), "layers": np.int64(c["layers"]),
            "onehot": np.int64(1), "rev": np.int64(0), "snr": np.asarray(SNRS), "train_snr": np.float64(c["snr_train"]),
-           "curriculum": np.asarray(c["curriculum"], np.int64), "train_batch": np.int64(c["batch"]),
+           "pac": np.int64(c["code"] == "PAC"), "profile": np.bytes_(c["profile"]),
+           # (K, steps, trainer) per stage; trainer 0 = the reference's rnn_all.py (CPU), 1 = train_crisp_gpu.py
+           "curriculum": np.asarray([(k, n, int(w == "gpu")) for k, n, w in c["curriculum"]], np.int64),
+           "ref_lr": np.float64(c["ref_lr"]), "train_batch": np.int64(c["batch"]),
            "n_dec": np.int64(c["n_dec"]), "seed_dec": np.int64(c["seed_dec"])}
     out.update({"w." + k: v.detach().numpy() for k, v in net.state_dict().items()})
 
@@ -173,7 +183,10 @@ def evaluate(name, c, ckpt):
             ke += int((e > 0).sum())
             se += int((e * e).sum())
             if sn < c["n_sc"]:
-                _, hat = code.sc_decode_new(y, snr)
+                if c["code"] == "Polar":
+                    _, hat = code.sc_decode_new(y, snr)
+                else:
+                    _, hat, _ = code.pac_sc_decode(y, snr)
                 es = (hat != msg).sum(1)
                 sb += int(es.sum())
                 sk += int((es > 0).sum())
@@ -196,16 +209,18 @@ def main():
     ap.add_argument("cases", nargs="*", default=list(CASES))
     ap.add_argument("--workdir", default="/tmp/npd_train")
     ap.add_argument("--eval-only", action="store_true", help="skip training (checkpoints already in --workdir)")
+    ap.add_argument("--gpu-weights", default=None, help="weights after the GPU stages (default train_state/<case>.net.pt)")
+    ap.add_argument("--threads", type=int, default=None, help="torch threads for the evaluation (training: OMP_NUM_THREADS)")
     args = ap.parse_args()
     if not os.path.isdir(REF):
         raise SystemExit("reference not present: fixtures can only be generated in the build container")
-    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    torch.set_num_threads(args.threads or min(8, os.cpu_count() or 1))
     for name in args.cases:
         c = CASES[name]
         lastK = c["curriculum"][-1][0]
-        nK = sum(1 for k, _ in c["curriculum"] if k == lastK)
+        nK = sum(1 for k, _, w in c["curriculum"] if k == lastK and w == "ref")
         ckpt = os.path.join(args.workdir, name, f"K{lastK}.pt" if nK == 1 else f"K{lastK}_{nK}.pt") \
-            if args.eval_only else train(name, c, args.workdir)
+            if args.eval_only else train(name, c, args.workdir, args.gpu_weights)
         evaluate(name, c, ckpt)
 
 

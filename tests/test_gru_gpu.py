@@ -76,10 +76,12 @@ def test_gru_genie_frozen_values():
 
 @pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev"])
 def test_gru_decode_fp16x3_meets_fp32_tolerance(name):
-    """The scaled fp16x3 split path (precision "fp16x3": hi + lo fp16 parts of weights x 2^8 and states x 2^8,
-    three v_mfma_f32_32x32x16_f16 products per multiply, fp32 accumulation) held to the FP32 path's bars on
+    """The fp16x3 split path (precision "fp16x3": hi + lo fp16 parts of weights and states, three fp16 MFMA
+    products per multiply, fp32 accumulation) held to the FP32 path's bars on
     the reference's golden words: logits within 2e-5, >= 99.9 % of information bits and >= 99 % of
-    codewords identical.  (The F <= 64 fixtures: the split kernels cover hidden sizes up to 64.)"""
+    codewords identical.  (The F <= 64 fixtures: the split kernels cover hidden sizes up to 64.)  F = 64, 2 layers,
+    N % 32 == 0 (Polar(64,32), PAC(128,64)) runs gru16p_kernel's unscaled split with the gate constants folded
+    into the weights (SPLIT 5); other shapes (the N = 16 fixture) the 32-codeword kernel's x 2^8-scaled split."""
     d = golden(f"{name}.npz")
     net, dec = build(d, "fp16x3")
     y = torch.from_numpy(d["y"]).to(DEV)
@@ -111,6 +113,26 @@ def test_gru_fp16x3_vs_oracle_ragged():
     assert np.abs(logits[same] - ol[same]).max() < LOGIT_ATOL
 
 
+def test_gru_fp16x3_small_weights_vs_oracle():
+    """The unscaled fp16x3 split (F = 64, 2 layers) keeps the lo parts of small weights and states as fp16
+    subnormals (absolute resolution 2^-24): with every parameter scaled by 1/16 (|w| mostly < 8e-3, so most lo
+    parts are subnormal) the logits still meet the fp32 bars against the C oracle."""
+    from oracle import oracle as O
+    from neural_polar_decoder_amd import reference_polar_code
+    d = golden("gru_polar_64_32.npz")
+    net, dec = build(d, "fp16x3")
+    sd = {k[2:]: (d[k] / 16).astype(np.float32) for k in d.files if k.startswith("w.")}
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    code = reference_polar_code(64, 32)
+    _, _, y = code.mc_generate(2048 + 5, 2.0, seed=13, device=DEV, want_msg=False)
+    out, logits = dec.decode(net, False, y, return_logits=True)
+    od, ol = O.gru_decode(y.cpu().numpy(), sd, 64, 64, 2, d["info"], onehot=True, want_logits=True)
+    out, logits = out.cpu().numpy(), logits.cpu().numpy()
+    same = (out == od).all(1)
+    assert same.mean() >= 0.99
+    assert np.abs(logits[same] - ol[same]).max() < LOGIT_ATOL
+
+
 # bf16 MFMA variants (not the reference's arithmetic; opt-in). Tolerances:
 #   bf16x3 (hi/lo split, ~2^-16 relative per product, fast exp2/rcp gates): logits within 2e-3 absolute
 #          on agreeing codewords, >= 99.5 % information-bit agreement, >= 97 % codeword agreement.
@@ -121,7 +143,7 @@ BF_TOL = {"bf16x3": (2e-3, 0.995, 0.97), "bf16": (None, 0.98, 0.85)}
 
 
 @pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
-@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64"])
+@pytest.mark.parametrize("name", ["gru_polar_64_32", "gru_pac_128_64", "gru_polar_16_8_noonehot_rev"])
 def test_gru_decode_bf16_golden(name, precision):
     d = golden(f"{name}.npz")
     net, dec = build(d, precision)

@@ -1,6 +1,5 @@
 """Child program for PMC passes on the F = 64 CRISP GRU kernels (rocprofv3 --pmc ... -- python3 tools/pmc_gru_child.py):
-2^18 Polar(64,32) words at 2 dB, fp32 and fp16x3 paths, 3 launches each (NPD_GRU16=0 selects the 32-codeword split
-kernel for the fp16x3 path)."""
+2^18 Polar(64,32) words at 2 dB, fp32 and fp16x3 paths, 3 launches each."""
 import sys
 
 import torch
