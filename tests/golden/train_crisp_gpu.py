@@ -12,8 +12,8 @@ the reference (it runs on the GPU box); the fixtures' parity claims rest on the 
 Restatement of rnn_all.py's training loop (rnn_all.py:1386-1440) for decoding_type y_input, onehot, GRU,
 teacher forcing ratio 1 (tfr_min = tfr_max = 1, run_crisp.sh:2):
   * per step: msg = 1 - 2 (rand < 0.5) (B, K); gt = ones (B, N), gt[:, info] = msg (rnn_all.py:1395-1397);
-    y = channel(encode(msg), snr_train) (:1399-1400; encode: this package's HIP encoder, bit-exact to
-    encode_plotkin / pac_encode; noise: sigma * randn);
+    y = channel(encode(msg), snr_train) (:1399-1400; encode: a torch restatement of encode_plotkin / pac_encode,
+    held to the oracle's bit-exact encoders by tests/test_trained_gru.py; noise: sigma * randn);
   * teacher forcing (rnn_all.py:436-450): N single-step GRU calls with input [y, onehot(prev)], prev = +1
     for step 0 and gt[:, i-1] after; the same recurrence as ONE nn.GRU call over the length-N sequence;
     decoded[:, i] = Linear(h1_i) (rnn_all.py:387-398);
@@ -40,7 +40,6 @@ import torch.nn as nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
-from neural_polar_decoder_amd import PAC, PolarCode  # noqa: E402
 from neural_polar_decoder_amd.codes import pac_info_positions, polar_info_positions  # noqa: E402
 from neural_polar_decoder_amd.rnn import RNN_decoder, RNN_Model  # noqa: E402
 from neural_polar_decoder_amd.utils import snr_db2sigma  # noqa: E402
@@ -49,17 +48,45 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from crisp_cases import CASES  # noqa: E402
 
 
-def make_code(c, K):
-    """Stage-K code of the curriculum: rnn_all.get_code(code, rate_profile, N, K) with --target_K = c['K']."""
+def plotkin(u):
+    """x = u F^{(x)n} in BPSK (XOR as product): stage d, blocks of 2^(d+1): left <- left * right (polar.py:128-148)."""
+    B, N = u.shape
+    x = u.clone()
+    s = 1
+    while s < N:
+        v = x.view(B, N // (2 * s), 2, s)
+        v[:, :, 0, :] = v[:, :, 0, :] * v[:, :, 1, :]
+        s *= 2
+    return x
+
+
+def pac_conv(v, taps=(2, 3, 5, 6)):
+    """PAC rate-1/1 convolution with g = 91 (pac_code.py:193-200): u_i = v_i prod_{j in taps} v_{i-j}, v_{<0} = +1."""
+    B, N = v.shape
+    vp = torch.cat([torch.ones(B, max(taps), device=v.device), v], 1)
+    u = v.clone()
+    for j in taps:
+        u = u * vp[:, max(taps) - j: max(taps) - j + N]
+    return u
+
+
+def make_code(c, K, device="cuda"):
+    """Stage-K code of the curriculum: rnn_all.get_code(code, rate_profile, N, K) with --target_K = c['K'].
+    Returns (info, encode) with encode(msg) -> x on msg's device (torch restatement of encode_plotkin /
+    pac_encode, checked against the oracle's bit-exact encoders by tests/test_trained_gru.py)."""
     N = c["N"]
     if c["code"] == "Polar":
         info = polar_info_positions(N, K, c["profile"], target_K=c["K"])
-        frozen = np.setdiff1d(np.arange(N), info)
-        code = PolarCode(int(np.log2(N)), K, F=frozen)
-        return code, info, code.encode_plotkin
-    code = PAC(argparse.Namespace(target_K=c["K"]), N, K, 91, rate_profile=c["profile"])
-    info = pac_info_positions(N, K, c["profile"], target_K=c["K"])
-    return code, info, code.pac_encode
+    else:
+        info = pac_info_positions(N, K, c["profile"], target_K=c["K"])
+    it = torch.as_tensor(info, device=device)
+    pac = c["code"] == "PAC"
+
+    def enc(msg):
+        u = torch.ones(msg.shape[0], N, device=msg.device)
+        u[:, it] = msg
+        return plotkin(pac_conv(u) if pac else u)
+    return info, enc
 
 
 def teacher_forced(net, y, gt):
@@ -74,16 +101,31 @@ def teacher_forced(net, y, gt):
 
 
 @torch.no_grad()
-def evaluate(net, c, K, snrs, n=1 << 14):
-    """BER / BLER of the fused HIP decoder (the product's eval path) at the stage's code."""
-    code, info, enc = make_code(c, K)
-    dec = RNN_decoder("y_input", c["N"], info, onehot=True)
+def evaluate(net, c, K, snrs, dev, n=1 << 14):
+    """BER / BLER at the stage's code: the fused HIP decoder (the product's eval path) on a GPU, the
+    reference's per-step loop (rnn_all.py:532-547, RNN_Model.forward) on the CPU."""
+    info, enc = make_code(c, K, dev)
+    it = torch.as_tensor(info, device=dev)
     net.eval()
     res = []
     for s in snrs:
-        msg = 1 - 2 * (torch.rand(n, K, device="cuda") < 0.5).float()
-        y = enc(msg) + snr_db2sigma(s) * torch.randn(n, c["N"], device="cuda")
-        d = dec.decode(net, False, y)[:, torch.as_tensor(info, device="cuda")]
+        msg = 1 - 2 * (torch.rand(n, K, device=dev) < 0.5).float()
+        y = enc(msg) + snr_db2sigma(s) * torch.randn(n, c["N"], device=dev)
+        if dev.type == "cuda":
+            d = RNN_decoder("y_input", c["N"], info, onehot=True).decode(net, False, y)[:, it]
+        else:
+            N = c["N"]
+            isinfo = np.zeros(N, bool)
+            isinfo[info] = True
+            dd = torch.ones(n, N)
+            hidden = torch.zeros(net.num_rnn_layers, n, net.feature_size)
+            for ii in range(N):
+                prev = torch.ones(n) if ii == 0 else dd[:, ii - 1].sign()
+                oh = torch.stack([(prev <= 0).float(), (prev > 0).float()], 1)
+                out, hidden = net(torch.cat([y.unsqueeze(1), oh.view(-1, 1, 2)], 2), hidden)
+                if isinfo[ii]:
+                    dd[:, ii] = out.squeeze().sign()
+            d = dd[:, it]
         e = (d != msg).sum(1)
         res.append((float(e.sum()) / (n * K), float((e > 0).float().mean())))
     net.train()
@@ -98,21 +140,26 @@ def main():
     ap.add_argument("--budget-s", type=float, default=1000.0)
     ap.add_argument("--eval-every", type=int, default=1000)
     ap.add_argument("--miopen", action="store_true", help="nn.GRU through MIOpen (default: PyTorch's native GRU)")
+    ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu")
+    ap.add_argument("--threads", type=int, default=None)
     args = ap.parse_args()
     torch.backends.cudnn.enabled = args.miopen
+    dev = torch.device(args.device)
+    if args.threads:
+        torch.set_num_threads(args.threads)
     c = CASES[args.case]
     stages = [(K, steps) for K, steps, who in c["curriculum"] if who == "gpu"]
     t_start = time.time()
     N, F, L = c["N"], c["F"], c["layers"]
-    net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).cuda()
+    net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).to(dev)
     st = {"stage": 0, "step": 0}
     if os.path.exists(args.state):
-        st = torch.load(args.state, map_location="cuda", weights_only=True)
+        st = torch.load(args.state, map_location=dev, weights_only=True)
         net.load_state_dict(st["net"])
         print(f"resume {args.case}: stage {st['stage']} step {st['step']}", flush=True)
     else:
         torch.manual_seed(c["seed_init"])
-        net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).cuda()  # PyTorch default init, as RNN_Model(...)
+        net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).to(dev)  # PyTorch default init, as RNN_Model(...)
     loss_fn = nn.MSELoss()
     last_save = time.time()
     last_print = time.time()
@@ -127,8 +174,8 @@ def main():
     while st["stage"] < len(stages):
         si = st["stage"]
         K, steps = stages[si]
-        code, info, enc = make_code(c, K)
-        info_t = torch.as_tensor(info, device="cuda")
+        info, enc = make_code(c, K, dev)
+        info_t = torch.as_tensor(info, device=dev)
         opt = torch.optim.AdamW(net.parameters(), lr=c["lr"])
         sched = torch.optim.lr_scheduler.StepLR(opt, c["lr_decay"], c["lr_gamma"])
         if st["step"] > 0 and "opt" in st:
@@ -139,10 +186,10 @@ def main():
         net.train()
         t0, s0 = time.time(), st["step"]
         for step in range(st["step"], steps):
-            msg = 1 - 2 * (torch.rand(c["batch"], K, device="cuda") < 0.5).float()
-            gt = torch.ones(c["batch"], N, device="cuda")
+            msg = 1 - 2 * (torch.rand(c["batch"], K, device=dev) < 0.5).float()
+            gt = torch.ones(c["batch"], N, device=dev)
             gt[:, info_t] = msg
-            y = enc(msg) + sigma * torch.randn(c["batch"], N, device="cuda")
+            y = enc(msg) + sigma * torch.randn(c["batch"], N, device=dev)
             decoded = teacher_forced(net, y, gt)
             loss = loss_fn(decoded[:, info_t], msg)
             loss.backward()
@@ -157,7 +204,7 @@ def main():
                       f"loss {loss.item():.5f} lr {sched.get_last_lr()[0]:.2e} ({rate:.1f} steps/s)", flush=True)
                 last_print = now
             if (step + 1) % args.eval_every == 0 or step == steps - 1:
-                r = evaluate(net, c, K, c["eval_snrs"])
+                r = evaluate(net, c, K, c["eval_snrs"], dev)
                 print("   eval " + " ".join(f"{s:g}dB BER {b:.4f} BLER {k:.4f}" for s, (b, k) in zip(c["eval_snrs"], r)),
                       flush=True)
             if now - t_start > args.budget_s:

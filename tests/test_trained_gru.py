@@ -33,3 +33,23 @@ def test_oracle_gru_trained_fixture(oracle, name):
         # N = 64, whose shorter curriculum leaves it at BER 0.33-0.36)
         assert (ref != msg[:n]).mean() < 0.42
         assert np.median(np.abs(d[f"logits_{si}"][:, info])) > 0.05
+
+
+def test_trainer_encoders_match_oracle(oracle):
+    """tests/golden/train_crisp_gpu.py's torch encoders (the GPU curriculum stages' data) == the oracle's bit-exact
+    encode_plotkin / pac_encode, at every stage code of the PAC(128,64) and Polar(64,32) curricula sampled."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from crisp_cases import CASES
+    from train_crisp_gpu import make_code
+    rng = np.random.default_rng(5)
+    for name, Ks in (("trained_crisp_64_32", (8, 20, 32)), ("trained_pac_128_64", (8, 37, 64))):
+        c = CASES[name]
+        for K in Ks:
+            info, enc = make_code(c, K, torch.device("cpu"))
+            msg = np.where(rng.random((300, K)) < 0.5, -1.0, 1.0).astype(np.float32)
+            x = enc(torch.from_numpy(msg)).numpy()
+            ref = oracle.encode_plotkin(msg, c["N"], info) if c["code"] == "Polar" else oracle.pac_encode(msg, c["N"], info)
+            assert np.array_equal(x, ref), (name, K)
