@@ -80,25 +80,31 @@ def gru_flop_per_cw(N, F):
 
 
 TRAINED_64_32 = os.path.join(ROOT, "tests", "golden", "trained_crisp_64_32.npz")
+TRAINED_PAC = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64.npz")
 
 
-def crisp_model(code, dev, precision="fp32"):
-    """The CRISP GRU (hidden 64, 2 layers, onehot y_input) of configs[2]: the Polar(64,32) decoder trained with
-    the reference's own training loop (tests/golden/gen_trained.py) when that fixture is present, else
-    PyTorch-default seeded weights.  Returns (net, decoder, description, fixture or None)."""
+def trained_or_seeded(code, path, info, dev, precision="fp32"):
+    """A CRISP GRU (hidden 64, 2 layers, onehot y_input): the trained fixture at `path` (tests/golden/gen_trained.py:
+    curriculum stages on the GPU, final stage by the reference's own training loop) when present, else PyTorch-default
+    seeded weights.  Returns (net, decoder, description, fixture or None)."""
     from neural_polar_decoder_amd.montecarlo import seeded_crisp
     from neural_polar_decoder_amd.rnn import RNN_Model, RNN_decoder
-    if os.path.exists(TRAINED_64_32):
-        d = np.load(TRAINED_64_32)
+    if os.path.exists(path):
+        d = np.load(path)
         N, F = int(d["N"]), int(d["F"])
         net = RNN_Model("GRU", N + 2, F, 1, int(d["layers"]), N, 0, 0).to(dev).eval()
         net.load_state_dict({k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w.")})
-        if not np.array_equal(d["info"], code.info_positions):
-            raise SystemExit("trained CRISP fixture is for another information set")
-        dec = RNN_decoder("y_input", N, code.info_positions, onehot=True, precision=precision)
-        return net, dec, "trained with the reference's training loop (tests/golden/trained_crisp_64_32.npz)", d
+        if not np.array_equal(d["info"], np.asarray(info)):
+            raise SystemExit(f"{path}: trained CRISP fixture is for another information set")
+        dec = RNN_decoder("y_input", N, np.asarray(info), onehot=True, precision=precision)
+        return net, dec, f"trained (tests/golden/{os.path.basename(path)})", d
     net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev, precision=precision)
     return net, dec, "seeded untrained weights (trained fixture absent)", None
+
+
+def crisp_model(code, dev, precision="fp32"):
+    """The CRISP GRU of configs[2] (Polar(64,32)): trained_or_seeded with the Polar(64,32) fixture."""
+    return trained_or_seeded(code, TRAINED_64_32, code.info_positions, dev, precision)
 
 
 def gru_vs_reference(fix, snrs, bit_err, blk_err, n_cw, K):
@@ -452,7 +458,6 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
     received words resident; CRISP GRU hidden 64 and PAC SC; one RCCL all-reduce of the counters."""
     import argparse as _ap
     from neural_polar_decoder_amd import PAC
-    from neural_polar_decoder_amd.montecarlo import seeded_crisp
     from neural_polar_decoder_amd.utils import count_errors
     code = PAC(_ap.Namespace(target_K=64), 128, 64, 91)
     cw0 = rank * B
@@ -479,9 +484,10 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
         cc = c.cpu().numpy()
         nb = 768 * B  # 4N + 4K bytes per codeword: y in, msg_hat out
         out["pac_sc"] = {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
-                         "avg_launch_ms": ms, "roofline": {"bound": "hbm", "achieved_gbs": nb / (ms / 1e3) / 1e9,
-                                                           "peak_gbs": HBM_PEAK_GBS,
-                                                           "frac": nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                         "avg_launch_ms": ms, "roofline": {"bound": "hbm", "achieved": nb / (ms / 1e3) / 1e9,
+                                                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                           "frac": nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                                           "algorithmic_bytes_per_launch": nb, "traffic": None},
                          "ber": {str(s): float(cc[i, 0]) / (world * B * 64) for i, s in enumerate(snrs)},
                          "bler": {str(s): float(cc[i, 1]) / (world * B) for i, s in enumerate(snrs)},
                          "config": "PAC(128,64) SC (pac_sc_decode, pac_code.py:534-573), 2^20 per SNR per GPU, 0-4 dB"}
@@ -505,7 +511,7 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
                                  "config": "PAC(128,64) fused Monte-Carlo sweep: message -> PAC encode -> AWGN -> SC -> "
                                            "count, 2^20 per SNR per GPU, 0-4 dB, one launch"}
     if do_gru:
-        net, dec = seeded_crisp(code, 64, 2, seed=0, device=dev)
+        net, dec, wdesc, fix = trained_or_seeded(code, TRAINED_PAC, code.B, dev)
         c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
 
         def gru_step():
@@ -520,7 +526,7 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
         n = world * B  # counted once per SNR (the timer's single call); the event pass does not count
         flop_cw = gru_flop_per_cw(128, 64)
         tf = flop_cw * B / (ms / 1e3) / 1e12
-        net16, dec16 = seeded_crisp(code, 64, 2, seed=0, device=dev, precision="fp16x3")
+        net16, dec16, _, _ = trained_or_seeded(code, TRAINED_PAC, code.B, dev, precision="fp16x3")
         dec16.decode(net16, False, ys[0][:64])
         ms16 = event_ms(lambda: dec16.decode(net16, False, ys[2]), 1, stream)
         out["pac_gru"] = {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3,
@@ -530,8 +536,10 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
                           "total_codewords": world * len(snrs) * B,
                           "ber": {str(s): float(cc[i, 0]) / (n * 64) for i, s in enumerate(snrs)},
                           "bler": {str(s): float(cc[i, 1]) / n for i, s in enumerate(snrs)},
-                          "config": "configs[3]: PAC(128,64) CRISP GRU hidden 64, 2 layers, fp32, seeded untrained "
-                                    "weights; 2^20 per SNR per GPU (2^23 at 8 GPUs), 0-4 dB, RCCL counter all-reduce"}
+                          "weights": wdesc,
+                          "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, 64),
+                          "config": "configs[3]: PAC(128,64) CRISP GRU hidden 64, 2 layers, fp32; 2^20 per SNR per GPU "
+                                    "(2^23 at 8 GPUs), 0-4 dB, RCCL counter all-reduce"}
     return out
 
 
@@ -618,13 +626,26 @@ def traffic_child(args):
     cnt = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     for _ in range(4):
         code.sc_decode_mc_sweep(yall, snrs, SEED, 0, cnt, msg_hat=hat)
+    del yall, hat
+    # the pac_sc leg's launch: PAC(128,64) streaming SC + counts + msg_hat, 2^20 words at 2 dB
+    import argparse as _ap
+    from neural_polar_decoder_amd import PAC
+    pac = PAC(_ap.Namespace(target_K=64), 128, 64, 91)
+    _, _, yp = pac.mc_generate(B, 2.0, SEED, 2, 0, device=dev, want_msg=False)
+    hp = torch.empty(B, 64, dtype=torch.float32, device=dev)
+    for _ in range(4):
+        pac.sc_decode_mc(yp, 2.0, SEED, 0, cnt[0], msg_hat=hp)
     torch.cuda.synchronize()
 
 
+PAC_KERNEL = "sc_decode_kernel<128"
+
+
 def pmc_traffic(args, timeout_s=240):
-    """HBM bytes per decode launch from rocprofv3 PMC counters, one counter per pass
-    (MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of wide coalesced streaming reads on
-    gfx950 -> doubled; WRITE_SIZE exact for 16-B/lane streaming stores; both in KiB)."""
+    """HBM bytes per launch of the headline decode kernel and of the pac_sc leg's kernel, from rocprofv3 PMC
+    counters, one counter per pass (MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of wide coalesced
+    streaming reads on gfx950 -> doubled; WRITE_SIZE exact for 16-B/lane streaming stores; both in KiB).
+    Returns ({kernel prefix: bytes per launch}, how)."""
     import csv
     import glob
     import shutil
@@ -632,7 +653,8 @@ def pmc_traffic(args, timeout_s=240):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not found"
-    vals = {}
+    names = (KERNEL_NAME.split("<")[0], PAC_KERNEL)
+    vals = {k: {} for k in names}
     tmp = tempfile.mkdtemp(prefix="npd_pmc_")
     env = dict(os.environ, TMPDIR="/tmp")
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -646,13 +668,15 @@ def pmc_traffic(args, timeout_s=240):
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
             return None, f"rocprofv3 rc={r.returncode}"
-        xs = [float(row["Counter_Value"]) for row in csv.DictReader(open(files[0]))
-              if KERNEL_NAME.split("<")[0] in row["Kernel_Name"] and row["Counter_Name"] == ctr]
-        if not xs:
-            return None, "kernel not found in PMC output"
-        vals[ctr] = sum(xs[1:]) / max(1, len(xs) - 1) if len(xs) > 1 else xs[0]  # skip the first (cold) launch
+        rows = list(csv.DictReader(open(files[0])))
+        for k in names:
+            xs = [float(row["Counter_Value"]) for row in rows if k in row["Kernel_Name"] and row["Counter_Name"] == ctr]
+            if not xs:
+                return None, f"kernel {k} not found in PMC output"
+            vals[k][ctr] = sum(xs[1:]) / max(1, len(xs) - 1) if len(xs) > 1 else xs[0]  # skip the first (cold) launch
     shutil.rmtree(tmp, ignore_errors=True)
-    return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024, "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 read)"
+    return ({k: (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024 for k, v in vals.items()},
+            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 read), one pass each")
 
 
 # ------------------------------------------------------------------------------------ main
@@ -799,8 +823,11 @@ def main():
     out.update(legs)
     if not args.no_traffic and world == 1:
         traffic, how = pmc_traffic(args)
-        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic"] = None if traffic is None else traffic[KERNEL_NAME.split("<")[0]]
         out["roofline"]["traffic_source"] = how
+        if "pac_sc" in out:
+            out["pac_sc"]["roofline"]["traffic"] = None if traffic is None else traffic[PAC_KERNEL]
+            out["pac_sc"]["roofline"]["traffic_source"] = how + "; the 2 dB launch of 2^20 words"
     if not args.no_cpu_baseline and world == 1:
         ys_host = [y[: 1 << 18].cpu().numpy() for y in ys]
         out["cpu_baseline"] = cpu_baseline(ys_host, snrs, code.info_positions, args.cpu_seconds)

@@ -72,10 +72,13 @@ def errors_ber(y_true, y_pred, mask=None):
     """Bit error rate (utils.py:17-25): mean of round(true) != round(pred) over the mask.
 
     Returns what the reference returns -- a float32 tensor of shape (1,) on ``y_true``'s device
-    (``sum(sum(x)) / torch.sum(mask)``) -- so the eval loops' ``.item()`` works unchanged.  The count is
-    exact (device uint64) and divided in fp32 like the reference's float sums.  An integer mask (the loops'
-    torch.ones(...).long()) is counted by npd_count_errors_masked -- sum(mask * err) / sum(mask), decided on
-    the device with no host read of the mask; a floating-point mask takes the reference's formula on the GPU."""
+    (``sum(sum(x)) / torch.sum(mask)``) -- so the eval loops' ``.item()`` works unchanged.  The counts are
+    exact (device int64), then each is rounded once to fp32 and divided in fp32: exact-then-rounded, not an fp32
+    accumulation.  Below 2^24 errors / mask elements per call both are exact and the result is the reference's
+    bit for bit; above it the reference's float32 sums drop low bits as they accumulate and ours is the correctly
+    rounded quotient of the true counts.  An integer mask (the loops' torch.ones(...).long()) is counted by
+    npd_count_errors_masked -- sum(mask * err) / sum(mask), decided on the device with no host read of the mask
+    (an all-ones mask costs the same single pass); a floating-point mask takes the reference's formula on the GPU."""
     if mask is not None:
         t = _lib.f32c(_lib.stage(y_true, "y_true"))
         if mask.dtype.is_floating_point or mask.dtype.is_complex:

@@ -111,7 +111,8 @@ def trained_fixture(name):
 def trained_words(d, si):
     """The fixture's decision words at SNR index si, regenerated exactly as gen_trained.py drew them through
     the reference (torch.manual_seed(seed_dec + si); msg = 1 - 2 (rand < 0.5); y = encode(msg) + sigma *
-    randn, polar.py:128-148, 201-207) -- the encoder is the oracle's (bit-exact +-1) -- and checked against
+    randn, polar.py:128-148, 201-207; PAC fixtures: pac_encode, pac_code.py:220-231) -- the encoder is the
+    oracle's (bit-exact +-1) -- and checked against
     the stored sha256 of y.  Returns (msg (B,K), y (B,N)) as float32 numpy arrays."""
     import hashlib
     import torch
@@ -119,7 +120,9 @@ def trained_words(d, si):
     N, K = int(d["N"]), int(d["K"])
     torch.manual_seed(int(d["seed_dec"]) + si)
     msg = 1.0 - 2.0 * (torch.rand(int(d["n_dec"]), K) < 0.5).float()
-    x = torch.from_numpy(O.encode_plotkin(msg.numpy(), N, d["info"]))
+    pac = "pac" in d.files and int(d["pac"]) == 1
+    enc = O.pac_encode if pac else O.encode_plotkin  # pac_code.py:220-224 / polar.py:128-148
+    x = torch.from_numpy(enc(msg.numpy(), N, d["info"]))
     sigma = 10 ** (-float(d["snr"][si]) * 1.0 / 20)
     y = x + sigma * torch.randn(x.shape, dtype=torch.float)
     yn = y.numpy()

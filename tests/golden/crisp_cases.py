@@ -31,6 +31,11 @@ CASES = {
                                 n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
     # PAC(128,64) 'RM' (configs[3], rnn_all.py:61 --code PAC): K = 8 .. 64 on the GPU, then the reference's loop
     "trained_pac_128_64": dict(_COMMON, code="PAC", profile="rev_RM", N=128, K=64, seed_init=12864,
-                               curriculum=_cur(8, 5000, 64, 1500, 30000, 400), ref_lr=2e-4,
+                               curriculum=_cur(8, 5000, 64, 800, 20000, 400), ref_lr=2e-4,
                                n_logit=256, n_sc=1 << 13, seed_dec=47, seed_mc=53),
+    # the same code on the easy-to-hard order (rate profile 'RM': stage K = the K highest-weight rows, run_rnn_e2h.sh's
+    # direction): the hard-first curriculum above stalls on PAC (BER 0.08-0.26 per bit even at 10 dB at K = 12)
+    "trained_pac_128_64_e2h": dict(_COMMON, code="PAC", profile="RM", N=128, K=64, seed_init=12865,
+                                   curriculum=_cur(8, 3000, 64, 800, 20000, 400), ref_lr=2e-4,
+                                   n_logit=256, n_sc=1 << 13, seed_dec=47, seed_mc=53),
 }

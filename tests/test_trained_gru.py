@@ -1,5 +1,6 @@
 """The oracle's GRU restatement at trained-model margins (CPU): decisions of oracle/ gru_decode on the trained
-fixture words (tests/golden/gen_trained.py: weights trained with the reference's own loop) against the
+fixture words (tests/golden/gen_trained.py: run_crisp.sh-shaped curricula, final stage by the reference's own
+training loop) against the
 reference's RNN_decoder.decode decisions, and its logits against the reference's.  Tolerance as for the
 seeded fixtures: logits within 2e-5 absolute on agreeing codewords; >= 99.9 % of information bits and
 >= 99 % of codewords identical."""
@@ -11,7 +12,7 @@ from conftest import trained_decisions, trained_fixture, trained_words
 LOGIT_ATOL = 2e-5
 
 
-@pytest.mark.parametrize("name", ["trained_crisp_32_16", "trained_crisp_64_32"])
+@pytest.mark.parametrize("name", ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64"])
 def test_oracle_gru_trained_fixture(oracle, name):
     d = trained_fixture(name)
     N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
@@ -29,10 +30,21 @@ def test_oracle_gru_trained_fixture(oracle, name):
         m = min(n, d[f"logits_{si}"].shape[0])
         assert np.abs(lg[:m][same[:m]] - d[f"logits_{si}"][:m][same[:m]]).max() < LOGIT_ATOL
         # the net is trained: its decisions beat a coin flip clearly (untrained nets sit at BER 0.5) and its
-        # information-position logits are away from zero (median |logit| 0.29-0.31 at N = 32, 0.08-0.09 at
-        # N = 64, whose shorter curriculum leaves it at BER 0.33-0.36)
-        assert (ref != msg[:n]).mean() < 0.42
-        assert np.median(np.abs(d[f"logits_{si}"][:, info])) > 0.05
+        # information-position logits are away from zero (untrained nets: median |logit| ~1e-2)
+        assert (ref != msg[:n]).mean() < 0.25
+        assert np.median(np.abs(d[f"logits_{si}"][:, info])) > 0.3
+    # ... and it decodes: the reference's own Monte-Carlo BLER is below 0.5 at two or more SNR points of 0-4 dB,
+    # so the BER-curve tolerance (tests/test_trained_gru_gpu.py: +-0.05 dB where BLER is in [1e-3, 0.9]) has points
+    # to act on
+    ref_bler = np.asarray(d["mc_blk_err"], float) / int(d["mc_n"])
+    assert (ref_bler < 0.5).sum() >= 2, ref_bler
+    # provenance: the fixture's curriculum is the one tests/golden/crisp_cases.py states
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from crisp_cases import CASES
+    cur = [(k, n, int(w == "gpu")) for k, n, w in CASES[name]["curriculum"]]
+    assert [tuple(int(v) for v in r) for r in d["curriculum"]] == cur
 
 
 def test_trainer_encoders_match_oracle(oracle):

@@ -1,9 +1,10 @@
 """The fused CRISP GRU decoder (npd_gru_decode) at trained-model margins.
 
-Fixtures: tests/golden/trained_crisp_{32_16,64_32}.npz -- CRISP GRUs (hidden 64, 2 layers, onehot y_input)
-trained with the reference's own training loop (rnn_all.py run as-is over a K curriculum) by
-tests/golden/gen_trained.py, the reference's decisions and logits on 4096 words per SNR (0..4 dB) and its
-Monte-Carlo BER/BLER curve (2^20 words per SNR through RNN_decoder.decode on the CPU).
+Fixtures: tests/golden/trained_{crisp_32_16,crisp_64_32,pac_128_64}.npz -- CRISP GRUs (hidden 64, 2 layers, onehot
+y_input) trained over run_crisp.sh-shaped K + 1 curricula (tests/golden/crisp_cases.py; Polar(32,16) entirely with
+the reference's own rnn_all.py, the others' early stages on the GPU and their final stage with rnn_all.py), the
+reference's decisions and logits on 4096 words per SNR (0..4 dB) and its Monte-Carlo BER/BLER curve (2^20 words
+per SNR through RNN_decoder.decode on the CPU), by tests/golden/gen_trained.py.
 
 Stated tolerance for the neural path (the north_star's "within a stated BER tolerance"):
   (a) decisions on the fixture words: >= 99.9 % of information bits and >= 99 % of codewords identical to
@@ -12,7 +13,8 @@ Stated tolerance for the neural path (the north_star's "within a stated BER tole
   (b) Monte-Carlo at 2^20 words per SNR (Philox words, independent of the reference's torch draws): BLER and
       BER within 4 two-sample standard errors of the reference's curve (BLER binomial; BER with the
       per-codeword bit-error variance from both sides), and the BLER curve's horizontal offset from the
-      reference's within +-0.05 dB at every point with BLER >= 1e-3 (standard error there ~0.01 dB).
+      reference's within +-0.05 dB at every point whose reference BLER is in [1e-3, 0.9] (standard error there
+      ~0.01 dB); at least two such points must exist, so the dB bar always runs.
 """
 import numpy as np
 import pytest
@@ -23,7 +25,7 @@ from conftest import db_offsets, trained_decisions, trained_fixture, trained_wor
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 LOGIT_ATOL = 2e-5
-CASES = ["trained_crisp_32_16", "trained_crisp_64_32"]
+CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64"]
 
 
 def build(d, precision="fp32"):
@@ -55,10 +57,10 @@ def test_trained_gru_decisions_match_reference(name, precision):
         assert err < LOGIT_ATOL, (float(d["snr"][si]), err)
 
 
-def mc_counts(code, net, dec, snrs, n, seed, batch=1 << 18):
+def mc_counts(code, info, net, dec, snrs, n, seed, batch=1 << 18):
     """bit errors, block errors and sum of squared per-codeword bit errors per SNR, HIP decoder on Philox
     words (npd_mc_generate), counted on the device."""
-    info = torch.as_tensor(np.asarray(code.info_positions), device=DEV)
+    info = torch.as_tensor(np.asarray(info), device=DEV)
     out = []
     for si, s in enumerate(snrs):
         be = bl = sq = 0
@@ -73,17 +75,30 @@ def mc_counts(code, net, dec, snrs, n, seed, batch=1 << 18):
     return out
 
 
+def fixture_code(d):
+    """The fixture's code object (product package) and its information set."""
+    import argparse
+    from neural_polar_decoder_amd import PAC, reference_polar_code
+    N, K = int(d["N"]), int(d["K"])
+    if "pac" in d.files and int(d["pac"]) == 1:
+        code = PAC(argparse.Namespace(target_K=K), N, K, 91)
+        info = np.asarray(code.B)
+    else:
+        code = reference_polar_code(N, K)
+        info = np.asarray(code.info_positions)
+    assert np.array_equal(info, d["info"])
+    return code, info
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_trained_gru_ber_curve_matches_reference(name):
-    from neural_polar_decoder_amd import reference_polar_code
     d = trained_fixture(name)
     net, dec = build(d)
-    N, K = int(d["N"]), int(d["K"])
-    code = reference_polar_code(N, K)
-    assert np.array_equal(np.asarray(code.info_positions), d["info"])
+    K = int(d["K"])
+    code, info = fixture_code(d)
     snrs = [float(s) for s in d["snr"]]
     n = 1 << 20
-    ours = mc_counts(code, net, dec, snrs, n, seed=2027)
+    ours = mc_counts(code, info, net, dec, snrs, n, seed=2027)
     nr = int(d["mc_n"])
     bler = []
     for si, s in enumerate(snrs):
@@ -98,10 +113,10 @@ def test_trained_gru_ber_curve_matches_reference(name):
         bler.append(p)
     ref_bler = [int(x) / nr for x in d["mc_blk_err"]]
     offs = db_offsets(snrs, bler, snrs, ref_bler, min_bler=1e-3)
+    checked = 0
     for s, o, pr in zip(snrs, offs, ref_bler):
-        # a dB offset is resolvable only where the curve falls: the N = 64 net's BLER stays above 0.99 on the
-        # whole grid (flat in SNR), so there the z-tests above are the bar
-        if o is not None and pr < 0.9:
-            assert abs(o) <= 0.05, (s, o)
-    # the trained decoder decodes: far below the coin-flip 0.5 of untrained weights at 2 dB
-    assert ours[2][0] / (n * K) < 0.4
+        # the dB offset is resolvable where the reference's curve falls: BLER in [1e-3, 0.9]
+        if 1e-3 <= pr <= 0.9:
+            assert o is not None and abs(o) <= 0.05, (s, o, pr)
+            checked += 1
+    assert checked >= 2, f"only {checked} SNR points with reference BLER in [1e-3, 0.9]: the dB bar cannot run"
