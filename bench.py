@@ -310,64 +310,87 @@ def mc_leg(code, snrs, B, cw0, world, timer, dev, ref_counts):
             "config": "Polar(64,32), 2^20 codewords per SNR per GPU, 0-4 dB, one fused launch per sweep"}
 
 
+PRECISION_JSON = os.path.join(ROOT, "profiles", "round4", "gru_precision.json")
+PMC_GRU_JSON = os.path.join(ROOT, "profiles", "round4", "pmc_gru_summary.json")
+
+
+def split_issue_bound(ms16, B, steps):
+    """Combined MFMA + VALU issue bound of gru16p_kernel from its committed PMC (profiles/round4/pmc_gru_summary.json):
+    the two serialise on a SIMD (profiles/round3/coissue.txt), so the kernel needs at least (MFMA busy + VALU busy)
+    cycles per SIMD.  Per wave-step cycles from the counters, scaled to this launch, over the clock the chip holds
+    (GRBM_GUI_ACTIVE / 8 / kernel time of the PMC run) and over the 2.4 GHz the spec peaks assume."""
+    if not os.path.exists(PMC_GRU_JSON):
+        return None
+    pm = json.load(open(PMC_GRU_JSON))
+    k = next((v for n, v in pm.items() if "gru16p_kernel" in n and isinstance(v, dict)), None)
+    if not k or "per_wave_step" not in k:
+        return None
+    ws = k["per_wave_step"]  # mfma_cycles, valu_cycles per 16-codeword wave and decoding step
+    simds = 1024
+    cycles = (ws["mfma_cycles"] + ws["valu_cycles"]) * (B / 16) * steps / simds
+    at_held = cycles / (k["clock_ghz"] * 1e9) * 1e3
+    at_spec = cycles / 2.4e9 * 1e3
+    return {"bound": "mfma + valu issue (serialised on the SIMD)", "pmc": "profiles/round4/pmc_gru_summary.json",
+            "mfma_cycles_per_wave_step": ws["mfma_cycles"], "valu_cycles_per_wave_step": ws["valu_cycles"],
+            "ceiling_ms_at_2.4GHz": at_spec, "ceiling_ms_at_held_clock": at_held, "held_clock_ghz": k["clock_ghz"],
+            "frac_at_2.4GHz": at_spec / ms16, "frac_at_held_clock": at_held / ms16}
+
+
 def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
     """The eval step the metric names (rnn_all.py:853-880): SC and the CRISP GRU decode the same words at every
-    SNR point and both are counted.  Its roofline is the GRU kernel's (fp32 MFMA; 99.8 % of the step)."""
+    SNR point and both are counted.  The GRU runs on the fp16x3 split kernel: its logit error against a float64
+    decoder equals the fp32 kernel's (profiles/round4/gru_precision.json, enforced by tests/test_gru_precision_gpu.py);
+    the fp32 kernel's step is reported beside it (fp32_path)."""
     from neural_polar_decoder_amd.utils import count_errors
-    net, dec, wdesc, fix = crisp_model(code, dev)
     c_sc = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
-    c_gru = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)  # decoded_SC_msg_bits, rnn_all.py:853
-        for si in range(len(snrs)):
-            count_errors(msg, dec.decode(net, False, yall[si]), c_gru[si], cols=code.info_positions)
-
-    t = timer(step, iters=2, warm=1)
-    # the GRU kernel alone, HIP events on its stream (one launch = one SNR point's 2^20 words)
-    ms = event_ms(lambda: dec.decode(net, False, yall[2]), 3, stream)
-    # the same step on the fp16x3 split path (held to the fp32 path's tolerance, tests/test_gru_gpu.py)
-    net16, dec16, _, _ = crisp_model(code, dev, precision="fp16x3")
-    c16 = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
-
-    def step16():
-        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)
-        for si in range(len(snrs)):
-            count_errors(msg, dec16.decode(net16, False, yall[si]), c16[si], cols=code.info_positions)
-
-    t16 = timer(step16, iters=2, warm=1)
-    ms16 = event_ms(lambda: dec16.decode(net16, False, yall[2]), 3, stream)
-    allreduce(c16, _sum(), world)
-    allreduce(c_gru, _sum(), world)
-    n = 3 * world * B
-    cg = c_gru.cpu().numpy()
-    c16n = c16.cpu().numpy()
     flop_cw = gru_flop_per_cw(N_CODE, 64)
-    tf = flop_cw * B / (ms / 1e3) / 1e12
-    tf16 = flop_cw * B / (ms16 / 1e3) / 1e12
-    fp16x3 = {"value": world * len(snrs) * B / t16, "ms_per_step": t16 * 1e3, "gru_avg_launch_ms": ms16,
-              "roofline": {"bound": "mfma + valu issue (serialised on the SIMD: profiles/round3/pmc_gru16_summary.json)",
-                           "kernel": "gru16p_kernel (16-codeword waves, v_mfma_f32_16x16x32_f16, 3 products per multiply)",
-                           "achieved": tf16, "peak": 2516.6, "unit": "TFLOP/s", "frac": tf16 / 2516.6,
-                           "algorithmic_flop_per_cw": flop_cw},
-              "gru_bit_errors_vs_fp32_path": [int(a) - int(b) for a, b in zip(c16n[:, 0], cg[:, 0])],
-              "gru_block_errors_vs_fp32_path": [int(a) - int(b) for a, b in zip(c16n[:, 1], cg[:, 1])],
-              "note": "GRU on the scaled hi+lo fp16 split (3 v_mfma_f32_32x32x16_f16 products per multiply, fp32 "
-                      "accumulation), held to the fp32 path's tolerance; not the reference's arithmetic, so the "
-                      "record's value stays the fp32 path"}
-    return {"value": world * len(snrs) * B / t, "unit": "codewords/s (each decoded by SC and by the GRU)",
-            "fp16x3_path": fp16x3,
-            "ms_per_step": t * 1e3, "weights": wdesc,
-            "roofline": {"bound": "mfma", "kernel": "gru_decode_kernel<64,2,4> (fp32 v_mfma_f32_32x32x2_f32)",
-                         "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "frac": tf / FP32_PEAK_TF,
-                         "traffic": None, "algorithmic_flop_per_cw": flop_cw, "codewords_per_launch": B,
-                         "avg_launch_ms": ms},
+    paths = {}
+    for prec in ("fp16x3", "fp32"):
+        net, dec, wdesc, fix = crisp_model(code, dev, precision=prec)
+        cg_dev = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+
+        def step():
+            code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)  # decoded_SC_msg_bits, rnn_all.py:853
+            for si in range(len(snrs)):
+                count_errors(msg, dec.decode(net, False, yall[si]), cg_dev[si], cols=code.info_positions)
+
+        t = timer(step, iters=2, warm=1)
+        # the GRU kernel alone, HIP events on its stream (one launch = one SNR point's 2^20 words)
+        ms = event_ms(lambda: dec.decode(net, False, yall[2]), 3, stream)
+        allreduce(cg_dev, _sum(), world)
+        paths[prec] = dict(t=t, ms=ms, cg=cg_dev.cpu().numpy() // 3, wdesc=wdesc, fix=fix)  # 3 counted passes
+    n = world * B
+    p16, p32 = paths["fp16x3"], paths["fp32"]
+    tf16 = flop_cw * B / (p16["ms"] / 1e3) / 1e12
+    tf32 = flop_cw * B / (p32["ms"] / 1e3) / 1e12
+    prec_table = json.load(open(PRECISION_JSON)) if os.path.exists(PRECISION_JSON) else None
+    cg = p16["cg"]
+    return {"value": world * len(snrs) * B / p16["t"], "unit": "codewords/s (each decoded by SC and by the GRU)",
+            "ms_per_step": p16["t"] * 1e3, "weights": p16["wdesc"],
+            "gru_precision": "fp16x3: hi + lo fp16 split, 3 v_mfma_f32_16x16x32_f16 products per multiply, fp32 "
+                             "accumulation (gru16p_kernel); logit error vs a float64 decoder equal to the fp32 kernel's",
+            "precision_evidence": None if prec_table is None else {
+                "source": "profiles/round4/gru_precision.json (tools/gru_precision.py)",
+                "abs_logit_error_vs_float64": {k: {q: v[q] for q in ("p50", "p99", "p99.9", "max", "cw_flips")}
+                                               for k, v in prec_table["impls"].items()},
+                "words": prec_table["words"]},
+            "roofline": dict({"kernel": "gru16p_kernel<5> (16-codeword waves, fp16x3)", "achieved": tf16,
+                              "unit": "TFLOP/s", "peak_fp16_dense": 2516.6, "frac_of_fp16_peak": tf16 / 2516.6,
+                              "algorithmic_flop_per_cw": flop_cw, "codewords_per_launch": B,
+                              "avg_launch_ms": p16["ms"]}, **(split_issue_bound(p16["ms"], B, N_CODE) or {})),
             "gru_ber": {str(s): float(cg[i, 0]) / (n * K_CODE) for i, s in enumerate(snrs)},
             "gru_bler": {str(s): float(cg[i, 1]) / n for i, s in enumerate(snrs)},
-            "gru_vs_reference": gru_vs_reference(fix, snrs, cg[:, 0], cg[:, 1], n, K_CODE),
+            "gru_vs_reference": gru_vs_reference(p16["fix"], snrs, cg[:, 0], cg[:, 1], n, K_CODE),
+            "gru_errors_fp32_minus_fp16x3": {"bits": [int(a) - int(b) for a, b in zip(p32["cg"][:, 0], cg[:, 0])],
+                                             "blocks": [int(a) - int(b) for a, b in zip(p32["cg"][:, 1], cg[:, 1])]},
+            "fp32_path": {"value": world * len(snrs) * B / p32["t"], "ms_per_step": p32["t"] * 1e3,
+                          "roofline": {"bound": "mfma", "kernel": "gru_decode_kernel<64,2> (fp32 v_mfma_f32_32x32x2_f32)",
+                                       "achieved": tf32, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
+                                       "frac": tf32 / FP32_PEAK_TF, "avg_launch_ms": p32["ms"]},
+                          "gru_ber": {str(s): float(p32["cg"][i, 0]) / (n * K_CODE) for i, s in enumerate(snrs)}},
             "config": "configs[1]+[2]: Polar(64,32), 2^20 words per SNR per GPU, 0-4 dB; SC sweep launch + 5 CRISP "
-                      "GRU (hidden 64, 2 layers, fp32) decodes + device counts"}
+                      "GRU (hidden 64, 2 layers) decodes + device counts"}
 
 
 def cpu_baseline_sc_gru(yall_host, snrs, info, net, budget_s):

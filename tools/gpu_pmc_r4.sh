@@ -7,3 +7,4 @@ PMC_CHILD=tools/pmc_gru_child.py PMC_OUT=gpurun_out/pmc_gru bash tools/gpu_pmc_k
 PMC_CHILD=tools/pmc_pac.py PMC_OUT=gpurun_out/pmc_pac bash tools/gpu_pmc_k.sh FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE"
 python3 tools/pmc_summary.py gpurun_out/pmc_gru > gpurun_out/pmc_gru/summary.json
 python3 tools/pmc_summary.py gpurun_out/pmc_pac > gpurun_out/pmc_pac/summary.json
+python3 tools/pmc_gru_r4.py gpurun_out/pmc_gru > gpurun_out/pmc_gru/pmc_gru_summary.json
