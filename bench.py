@@ -627,7 +627,49 @@ def conv_leg(dev, rank, world, timer, batch=8192):
     tf = flop_cw * batch / (ms / 1e3) / 1e12
     return {"value": world * batch / t, "unit": "codewords/s", "batch_per_gpu": batch, "avg_forward_ms": ms,
             "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
-            "frac": tf / FP32_PEAK_TF, "config": "configs[4]: Polar(256,128) convNet embed 128, fp32"}
+            "frac": tf / FP32_PEAK_TF, "config": "configs[4]: Polar(256,128) convNet embed 128, fp32, seeded weights",
+            "trained_scaled_down": trained_conv_curve(dev, rank, world)}
+
+
+TRAINED_CONV = os.path.join(ROOT, "tests", "golden", "trained_conv_64_22.npz")
+
+
+def trained_conv_curve(dev, rank, world, n=1 << 18):
+    """The trained conv fixture (embed 16, Polar(64,22), the reference's run_models.py over run_alt.sh's curriculum
+    shape): BER/BLER over 0-4 dB on Philox words, against the reference's own Monte-Carlo curve for the same weights."""
+    if not os.path.exists(TRAINED_CONV):
+        return None
+    import argparse as _ap
+    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.models import convNet
+    d = np.load(TRAINED_CONV)
+    N, K = int(d["N"]), int(d["K"])
+    net = convNet(_ap.Namespace(embed_dim=int(d["embed"]), max_len=N, N=N, dont_use_bias=False, dropout=0.0))
+    net.load_state_dict({k[2:]: torch.from_numpy(np.asarray(d[k])) for k in d.files if k.startswith("w.")})
+    net.eval()
+    code = reference_polar_code(N, K)
+    info = torch.as_tensor(d["info"], device=dev)
+    snrs = [float(x) for x in d["snr"]]
+    c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    sq = torch.zeros(len(snrs), dtype=torch.int64, device=dev)
+    for si, s_ in enumerate(snrs):
+        for off in range(0, n, 1 << 16):
+            msg, _, y = code.mc_generate(1 << 16, s_, SEED, si, rank * n + off, device=dev)
+            _, dec = net.logits(y)
+            e = (dec[:, info] != msg).sum(1).to(torch.int64)
+            c[si, 0] += e.sum()
+            c[si, 1] += (e > 0).sum()
+            sq[si] += (e * e).sum()
+    allreduce(c, _sum(), world)
+    cc = c.cpu().numpy()
+    tot = world * n
+    ref_bler = [int(x) / int(d["mc_n"]) for x in d["mc_blk_err"]]
+    bler = [float(cc[i, 1]) / tot for i in range(len(snrs))]
+    return {"weights": "tests/golden/trained_conv_64_22.npz", "words_per_snr": tot,
+            "ber": {str(s_): float(cc[i, 0]) / (tot * K) for i, s_ in enumerate(snrs)},
+            "bler": {str(s_): b for s_, b in zip(snrs, bler)},
+            "bler_reference": {str(s_): b for s_, b in zip(snrs, ref_bler)},
+            "bler_db_offset_vs_reference": {str(s_): o for s_, o in zip(snrs, db_offsets(snrs, bler, snrs, ref_bler))}}
 
 
 # ------------------------------------------------------------------------------------ PMC traffic

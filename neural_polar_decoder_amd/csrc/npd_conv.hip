@@ -37,7 +37,15 @@ struct LayerDesc {
     int64_t woff;   // offset (floats) of the permuted weights in the device image
     int64_t boff;   // offset of the bias
     int ksteps;     // ceil(7*cin / 2)
+    // fp16x3 split (precision 3, cin > 1): weight image offset (floats) and the accumulator descale 2^-(SW + SA)
+    int64_t soff;
+    float descale;
 };
+
+// fp16x3: activations are split as fp16(a 2^SA) + fp16(a 2^SA - hi) when staged (SA = 4: |a| up to 4094 before
+// fp16 overflows, lo normal for |a| >= 2^-7, below that lo's absolute resolution is 2^-28); the weights of each layer
+// are scaled by 2^SW on the host so that max |w| 2^SW is in [2^12, 2^13) (hi and lo normal for |w| >= max |w| 2^-11)
+constexpr int kSplitSA = 4;
 
 __device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
 
@@ -133,6 +141,114 @@ __global__ __launch_bounds__(256) void conv_layer_kernel(const float* __restrict
                 v += rv;
             }
             *reinterpret_cast<f4*>(out + o) = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ conv layer, fp16x3
+// precision 3 (cin > 1): the same implicit GEMM on v_mfma_f32_32x32x16_f16 with hi + lo fp16 operands, three
+// products per multiply (hi.hi + hi.lo + lo.hi), fp32 accumulation -- 16 channels of one tap per MFMA triple instead
+// of 8 fp32 MFMAs of 2 channels: 96 against 512 MFMA cycles per tap-group.  32x32x16 operand map (lane l, r = l&31,
+// h = l>>5): A[row r][k = 8h + j], B[k = 8h + j][col r], j = 0..7; k-step s of tap t covers channels 16s + k.
+// The slab is split once when staged: LDS holds a hi plane and a lo plane of fp16 rows [position][channel] of stride
+// CSH = cin16 + 8 (cin16 = cin rounded up to 16, the pad channels zero), so a B fragment (8 channels) is one
+// ds_read_b128 per plane.  Each wave owns 32 output channels x P position tiles: an A fragment pair (global, 2 x 16 B)
+// feeds P MFMA triples, which divides the weight stream by P.  Block: 2 (co) x 2 (position) waves, 64 P positions.
+// Epilogue (registers 4q..4q+3 = 4 consecutive channels, as conv_layer_kernel) after the exact descale 2^-(SW+SA).
+typedef _Float16 hf8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f16v mfma16(const hf8& a, const hf8& b, const f16v& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void conv_layer_split_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                               const float* __restrict__ res, const f4* __restrict__ wimg,
+                                                               const float* __restrict__ bias, int cin, int cout, int N,
+                                                               int dil, int do_res, float descale) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 slab16[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    constexpr int PT = 64 * P;  // positions per block
+    const int l0 = blockIdx.x * PT;
+    const int64_t b = blockIdx.z;
+    const int halo = 3 * dil;
+    const int W = PT + 2 * halo;
+    const int cin16 = (cin + 15) & ~15;
+    const int CSH = cin16 + 8;
+    _Float16* const hiP = slab16;
+    _Float16* const loP = slab16 + (size_t)W * CSH;
+    {
+        // stage + split: 4 channels per element (cin is a multiple of 8), pad channels of each row zeroed
+        const int c4n = cin >> 2, c4p = cin16 >> 2;
+        const f4* inb = reinterpret_cast<const f4*>(in + b * (int64_t)N * cin);
+        for (int e = tid; e < W * c4p; e += 256) {
+            const int p = e / c4p, c4 = e - p * c4p;
+            const int l = l0 - halo + p;
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (c4 < c4n && l >= 0 && l < N) v = inb[(int64_t)l * c4n + c4];
+            hf4 hi, lo;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float x = v[j] * (float)(1 << kSplitSA);
+                hi[j] = (_Float16)x;
+                lo[j] = (_Float16)(x - (float)hi[j]);
+            }
+            *reinterpret_cast<hf4*>(hiP + p * CSH + 4 * c4) = hi;
+            *reinterpret_cast<hf4*>(loP + p * CSH + 4 * c4) = lo;
+        }
+    }
+    __syncthreads();
+    const int co_sub = wave & 1, pos_sub = wave >> 1;
+    const int co_t32 = blockIdx.y * 2 + co_sub;  // 32-channel tile index
+    const int ng = cin16 >> 4;                   // 16-channel k-steps per tap
+    f16v acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // A fragments: [t32][tap][s][part][lane] 16 B
+    const f4* wq = wimg + (int64_t)co_t32 * 7 * ng * 128 + lane;
+    f4 whn = wq[0], wln = wq[64];
+    const int pbase = pos_sub * 32 * P + col;  // this lane's position column within the block, tile 0
+    for (int t = 0; t < 7; ++t) {
+        for (int g = 0; g < ng; ++g) {
+            const hf8 ah = __builtin_bit_cast(hf8, whn), al = __builtin_bit_cast(hf8, wln);
+            const int nxt = t * ng + g + 1;
+            if (nxt < 7 * ng) {
+                whn = wq[(int64_t)nxt * 128];
+                wln = wq[(int64_t)nxt * 128 + 64];
+            }
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const int off = (pbase + 32 * p + dil * t) * CSH + 16 * g + 8 * h;
+                const hf8 bh = *reinterpret_cast<const hf8*>(hiP + off);
+                const hf8 bl = *reinterpret_cast<const hf8*>(loP + off);
+                acc[p] = mfma16(ah, bh, acc[p]);
+                acc[p] = mfma16(ah, bl, acc[p]);
+                acc[p] = mfma16(al, bh, acc[p]);
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int l = l0 + pos_sub * 32 * P + 32 * p + col;
+        if (l >= N) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int co = co_t32 * 32 + 8 * q + 4 * h;
+            if (co < cout) {
+                const int64_t o = (b * N + l) * (int64_t)cout + co;
+                const f4 bb = *reinterpret_cast<const f4*>(bias + co);
+                f4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(acc[p][4 * q + e], descale, bb[e]));
+                if (do_res) {
+                    const f4 rv = *reinterpret_cast<const f4*>(res + o);
+                    v += rv;
+                }
+                *reinterpret_cast<f4*>(out + o) = v;
+            }
         }
     }
 }
@@ -270,7 +386,7 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
     NPD_ARG(weights != nullptr, "npd_conv_create: weights is NULL");
     NPD_ARG(N >= 64 && N <= 1024 && N % 64 == 0, "npd_conv_create: N must be a multiple of 64 in [64, 1024]");
     NPD_ARG(embed >= 16 && embed <= 512 && embed % 16 == 0, "npd_conv_create: embed must be a multiple of 16 in [16, 512]");
-    NPD_ARG(precision == 0, "npd_conv_create: only fp32 (precision 0) is built");
+    NPD_ARG(precision == 0 || precision == 3, "npd_conv_create: precision must be 0 (fp32) or 3 (fp16x3 conv layers)");
     const int E = embed;
     // host weights in state_dict order: (w, b) per conv layer, then 3 x (w, b) Linear, then LN (g, b)
     int64_t expect = 0;
@@ -322,6 +438,34 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
                                 const int cc = (l >> 5) * (ci / 2) + 4 * g + e;
                                 img[L.woff + ((((int64_t)t32 * 7 + t) * ng + g) * 64 + l) * 4 + e] =
                                     row < co ? w[((int64_t)row * ci + cc) * 7 + t] : 0.0f;
+                            }
+        }
+        if (precision == 3 && ci > 1) {
+            // fp16x3 A fragments [t32][tap][s][part hi/lo][lane][8 x fp16]: lane (r, hh), element j = W[row][16s + 8hh + j][t]
+            // x 2^SW, split hi = fp16(v), lo = fp16(v - hi)
+            float m = 0.0f;
+            for (int64_t i = 0; i < (int64_t)co * ci * 7; ++i) m = fmaxf(m, fabsf(w[i]));
+            const int sw = m > 0.0f ? 12 - (int)floorf(log2f(m)) : 0;
+            const float sc = ldexpf(1.0f, sw);
+            L.descale = ldexpf(1.0f, -(sw + kSplitSA));
+            const int ng = (ci + 15) / 16;
+            while (img.size() % 4) img.push_back(0.0f);
+            L.soff = (int64_t)img.size();
+            const size_t n16 = (size_t)(co_pad / 32) * 7 * ng * 2 * 64 * 8;
+            img.resize(img.size() + n16 / 2, 0.0f);
+            uint16_t* u16 = reinterpret_cast<uint16_t*>(img.data() + L.soff);
+            for (int t32 = 0; t32 < co_pad / 32; ++t32)
+                for (int t = 0; t < 7; ++t)
+                    for (int g = 0; g < ng; ++g)
+                        for (int l = 0; l < 64; ++l)
+                            for (int j = 0; j < 8; ++j) {
+                                const int row = 32 * t32 + (l & 31), cc = 16 * g + 8 * (l >> 5) + j;
+                                const float v = (row < co && cc < ci) ? w[((int64_t)row * ci + cc) * 7 + t] * sc : 0.0f;
+                                const _Float16 hi = (_Float16)v;
+                                const _Float16 lo = (_Float16)(v - (float)hi);
+                                const size_t e = ((((size_t)(t32 * 7 + t) * ng + g) * 2) * 64 + l) * 8 + j;
+                                memcpy(&u16[e], &hi, 2);
+                                memcpy(&u16[e + 64 * 8], &lo, 2);
                             }
         }
         p += (int64_t)co * ci * 7;
@@ -433,6 +577,12 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
     if (!attr) {
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
+        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    163840));
+        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    163840));
+        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    163840));
         attr = true;
     }
     for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -458,7 +608,24 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             if (L.cin == 1)
                 hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res);
-            else
+            else if (c->precision == 3) {
+                // positions per block 64 P: the largest P in {4, 2, 1} with 64 P <= N whose two fp16 slab planes fit
+                const int cs = ((L.cin + 15) & ~15) + 8;
+                int P = 4;
+                while (P > 1 && (64 * P > N || (size_t)2 * (64 * P + 2 * halo) * cs * 2 > 160 * 1024)) P >>= 1;
+                const size_t ls = (size_t)2 * (64 * P + 2 * halo) * cs * 2;
+                dim3 gs((N + 64 * P - 1) / (64 * P), (L.cout + 63) / 64, (unsigned)nb);
+                const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff);
+                if (P == 4)
+                    hipLaunchKernelGGL(conv_layer_split_kernel<4>, gs, dim3(256), ls, s, in, o, rsrc, wi, c->img + L.boff,
+                                       L.cin, L.cout, N, L.dil, L.res, L.descale);
+                else if (P == 2)
+                    hipLaunchKernelGGL(conv_layer_split_kernel<2>, gs, dim3(256), ls, s, in, o, rsrc, wi, c->img + L.boff,
+                                       L.cin, L.cout, N, L.dil, L.res, L.descale);
+                else
+                    hipLaunchKernelGGL(conv_layer_split_kernel<1>, gs, dim3(256), ls, s, in, o, rsrc, wi, c->img + L.boff,
+                                       L.cin, L.cout, N, L.dil, L.res, L.descale);
+            } else
                 hipLaunchKernelGGL(conv_layer_kernel<false>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res);
             int rc = launch_check("conv_layer_kernel launch");

@@ -17,8 +17,17 @@ from . import _lib
 
 
 class convNet(nn.Module):
-    def __init__(self, config):
+    """models.convNet.  ``precision`` (keyword, not in the reference): "fp32" (default; exact fp32 FMA chains on
+    v_mfma_f32_32x32x2_f32) or "fp16x3" (the conv layers with cin > 1 on v_mfma_f32_32x32x16_f16 with hi + lo fp16
+    operands, three products per multiply, fp32 accumulation; FC layers and LayerNorm stay fp32)."""
+
+    PRECISIONS = {"fp32": 0, "fp16x3": 3}
+
+    def __init__(self, config, precision="fp32"):
         super().__init__()
+        if precision not in self.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(self.PRECISIONS)}")
+        self.precision = precision
         self.hidden_dim = config.embed_dim
         self.input_len = config.max_len
         self.output_len = config.N
@@ -62,14 +71,16 @@ class convNet(nn.Module):
         return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
 
     def _get_handle(self, device):
-        key = (str(device), tuple(p._version for p in self.parameters()), tuple(p.data_ptr() for p in self.parameters()))
+        key = (str(device), self.precision, tuple(p._version for p in self.parameters()),
+               tuple(p.data_ptr() for p in self.parameters()))
         if self._handle is None or self._hkey != key:
             W = self._packed()
             out = ctypes.c_void_p()
             L = _lib.load()
             with torch.cuda.device(device):
                 _lib.check(L.npd_conv_create(int(self.output_len), int(self.hidden_dim), W.ctypes.data_as(ctypes.c_void_p),
-                                             int(W.size), 0, ctypes.byref(out)), "npd_conv_create")
+                                             int(W.size), self.PRECISIONS[self.precision], ctypes.byref(out)),
+                           "npd_conv_create")
             if self._handle is not None:
                 L.npd_conv_destroy(self._handle)
             self._handle, self._hkey = out, key

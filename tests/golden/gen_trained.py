@@ -57,21 +57,33 @@ def y_digest(y: np.ndarray) -> str:
 
 
 def train(name, c, workdir, gpu_weights=None):
-    """Run the reference's training script over the curriculum's "ref" stages; returns the final checkpoint
-    path.  A curriculum that starts with "gpu" stages continues from their weights (train_crisp_gpu.py's
-    --out file, default train_state/<name>.net.pt)."""
+    """Run the reference's training script over the curriculum's "ref" stages, in order; returns the final
+    checkpoint path.  A contiguous block of "gpu" stages (train_crisp_gpu.py) sits between the ref stages before it
+    (whose final weights are handed to the GPU trainer as train_state/<name>.init.pt) and those after it, which
+    continue from the GPU trainer's --out file (default train_state/<name>.net.pt)."""
     wd = os.path.join(workdir, name)
     os.makedirs(wd, exist_ok=True)
     prev = None
-    if any(who == "gpu" for _, _, who in c["curriculum"]):
-        prev = gpu_weights or os.path.join(TRAIN_STATE, f"{name}.net.pt")
-        if not os.path.exists(prev):
-            raise SystemExit(f"{name}: GPU curriculum stages not run yet ({prev} missing; tests/golden/train_crisp_gpu.py)")
     seen = {}
     path = None
+    gpu_done = False
     for K, steps, who in c["curriculum"]:
-        if who != "ref":
+        if who == "gpu":
+            if gpu_done:
+                continue
+            if prev is not None:
+                init = os.path.join(TRAIN_STATE, f"{name}.init.pt")
+                if not os.path.exists(init):
+                    os.makedirs(TRAIN_STATE, exist_ok=True)
+                    torch.save(torch.load(prev, map_location="cpu", weights_only=True), init)
+            prev = gpu_weights or os.path.join(TRAIN_STATE, f"{name}.net.pt")
+            if not os.path.exists(prev):
+                raise SystemExit(f"{name}: GPU curriculum stages not run yet ({prev} missing; run "
+                                 f"tests/golden/train_crisp_gpu.py {name}"
+                                 + (f" --init {TRAIN_STATE}/{name}.init.pt" if path else "") + ")")
+            gpu_done = True
             continue
+        lr = c["ref_lr"] if gpu_done else c["lr"]
         seen[K] = seen.get(K, 0) + 1  # a K repeated in the curriculum continues from the previous stage
         path = os.path.join(wd, f"K{K}.pt" if seen[K] == 1 else f"K{K}_{seen[K]}.pt")
         if os.path.exists(path) and os.path.exists(path + ".done"):
@@ -81,7 +93,7 @@ def train(name, c, workdir, gpu_weights=None):
                "--rate_profile", c["profile"], "--N", str(c["N"]), "--K", str(K), "--target_K", str(c["K"]),
                "--decoding_type", "y_input", "--onehot", "--rnn_type", "GRU", "--rnn_feature_size", str(c["F"]),
                "--rnn_depth", str(c["layers"]), "--num_steps", str(steps), "--batch_size", str(c["batch"]),
-               "--tfr_min", "1", "--tfr_max", "1", "--dec_train_snr", str(c["snr_train"]), "--lr", str(c["ref_lr"]),
+               "--tfr_min", "1", "--tfr_max", "1", "--dec_train_snr", str(c["snr_train"]), "--lr", str(lr),
                "--scheduler", "step", "--lr_decay", str(c["lr_decay"]), "--lr_decay_gamma", str(c["lr_gamma"]),
                "--print_freq", "250", "--test_batch_size", "2000", "--test_size", "2000", "--model_save_per", "100000",
                "--save_path", path, "--fresh"]

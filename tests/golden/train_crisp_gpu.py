@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--miopen", action="store_true", help="nn.GRU through MIOpen (default: PyTorch's native GRU)")
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu")
     ap.add_argument("--threads", type=int, default=None)
+    ap.add_argument("--init", default=None, help="weights ({'net': state_dict}) to start the first GPU stage from "
+                                                  "(the reference-loop stages before the GPU block)")
     args = ap.parse_args()
     torch.backends.cudnn.enabled = args.miopen
     dev = torch.device(args.device)
@@ -157,6 +159,9 @@ def main():
         st = torch.load(args.state, map_location=dev, weights_only=True)
         net.load_state_dict(st["net"])
         print(f"resume {args.case}: stage {st['stage']} step {st['step']}", flush=True)
+    elif args.init:
+        net.load_state_dict(torch.load(args.init, map_location=dev, weights_only=True)["net"])
+        print(f"init {args.case} from {args.init}", flush=True)
     else:
         torch.manual_seed(c["seed_init"])
         net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).to(dev)  # PyTorch default init, as RNN_Model(...)

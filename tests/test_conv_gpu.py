@@ -21,10 +21,10 @@ DEV = "cuda:0"
 ATOL = 1e-5
 
 
-def net_from(sd, embed, N):
+def net_from(sd, embed, N, precision="fp32"):
     from neural_polar_decoder_amd.models import convNet
     cfg = argparse.Namespace(embed_dim=embed, max_len=N, N=N, dont_use_bias=False, dropout=0.0)
-    net = convNet(cfg)
+    net = convNet(cfg, precision=precision)
     net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return net.eval()
 
@@ -88,3 +88,51 @@ def test_conv_forward_returns_input4(oracle):
     _, _, b4 = net.logits(torch.from_numpy(yb).to(DEV), want_input4=True)
     _, o4b = oracle.conv_forward(yb[::41], sd, want_input4=True)
     assert np.abs(b4.cpu().numpy()[::41] - o4b).max() < ATOL
+
+
+# ------------------------------------------------------------------------------------------- fp16x3 conv layers
+@pytest.mark.parametrize("name", ["conv_small_64", "conv_c5_256"])
+def test_conv_fp16x3_golden(name):
+    """precision "fp16x3" (conv layers with cin > 1 on the fp16 MFMA, hi + lo split, 3 products per multiply, fp32
+    accumulation) held to the fp32 path's bars on the reference's golden logits: within 1e-5, decisions identical
+    wherever the reference logit is farther than 1e-5 from zero (embed 16: 8-channel layers padded to 16; C5: embed
+    128, N 256, 4 position tiles per wave)."""
+    d = golden(f"{name}.npz")
+    if "w.layer_norm.weight" in d.files:
+        sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
+    else:
+        sd = conv_weights_from_seed(int(d["embed"]), int(d["N"]), int(d["seed"]))
+    net = net_from(sd, int(d["embed"]), int(d["N"]), precision="fp16x3")
+    lg, dec = net.logits(torch.from_numpy(d["y"]).to(DEV))
+    check(lg.cpu().numpy(), dec.cpu().numpy(), d["logits"])
+
+
+def test_conv_fp16x3_error_matches_fp32_against_float64(oracle):
+    """Precision study for the conv model (as tests/test_gru_precision_gpu.py for the GRU): |logit - float64 oracle|
+    of the fp16x3 path against the fp32 path's on the same words, C5 shape (embed 128, N 256, seeded weights) and the
+    trained embed-16 net: the fp16x3 error within 1.5 x the fp32 path's at p50 / p99 / p99.9 and its maximum within
+    2 x (products to 2^-22 relative against fp32's exact products; both accumulate in fp32)."""
+    rows = []
+    d5 = golden("conv_c5_256.npz")
+    sd5 = conv_weights_from_seed(int(d5["embed"]), int(d5["N"]), int(d5["seed"]))
+    rng = np.random.default_rng(11)
+    y5 = (np.where(rng.random((256, 256)) < 0.5, -1.0, 1.0) + 0.7 * rng.standard_normal((256, 256))).astype(np.float32)
+    rows.append((sd5, int(d5["embed"]), 256, y5))
+    import os
+    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trained_conv_64_22.npz")
+    if os.path.exists(tp):
+        dt = np.load(tp)
+        sdt = {k[2:]: np.asarray(dt[k]) for k in dt.files if k.startswith("w.")}
+        yt = (np.where(rng.random((4096, 64)) < 0.5, -1.0, 1.0) + 0.8 * rng.standard_normal((4096, 64))).astype(np.float32)
+        rows.append((sdt, int(dt["embed"]), 64, yt))
+    for sd, E, N, y in rows:
+        ref = oracle.conv_forward(y, sd).astype(np.float64)
+        errs = {}
+        for prec in ("fp32", "fp16x3"):
+            lg, _ = net_from(sd, E, N, precision=prec).logits(torch.from_numpy(y).to(DEV))
+            errs[prec] = np.abs(lg.cpu().numpy().astype(np.float64) - ref).ravel()
+        q32 = np.percentile(errs["fp32"], [50, 99, 99.9])
+        q16 = np.percentile(errs["fp16x3"], [50, 99, 99.9])
+        print(E, N, "fp32", q32, errs["fp32"].max(), "fp16x3", q16, errs["fp16x3"].max())
+        assert np.all(q16 <= 1.5 * q32), (E, N, q32, q16)
+        assert errs["fp16x3"].max() <= 2.0 * errs["fp32"].max(), (E, N)

@@ -26,11 +26,11 @@ ATOL = 1e-4  # trained weights: the reference's fp32 logits are up to 3.1e-5 fro
 NAME = "trained_conv_64_22"
 
 
-def net_from(d):
+def net_from(d, precision="fp32"):
     from neural_polar_decoder_amd.models import convNet
     N = int(d["N"])
     cfg = argparse.Namespace(embed_dim=int(d["embed"]), max_len=N, N=N, dont_use_bias=False, dropout=0.0)
-    net = convNet(cfg)
+    net = convNet(cfg, precision=precision)
     net.load_state_dict({k[2:]: torch.from_numpy(np.asarray(d[k])) for k in d.files if k.startswith("w.")})
     return net.eval()
 
@@ -50,9 +50,10 @@ def fixture_words(d, si):
     return msg.numpy(), y
 
 
-def test_trained_conv_decisions_match_reference():
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
+def test_trained_conv_decisions_match_reference(precision):
     d = trained_fixture(NAME)
-    net = net_from(d)
+    net = net_from(d, precision)
     N, K = int(d["N"]), int(d["K"])
     info = d["info"]
     for si in range(len(d["snr"])):
@@ -66,10 +67,11 @@ def test_trained_conv_decisions_match_reference():
         assert np.abs(lg.view(-1, N).cpu().numpy()[:m] - d[f"logits_{si}"]).max() < ATOL
 
 
-def test_trained_conv_ber_curve_matches_reference():
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
+def test_trained_conv_ber_curve_matches_reference(precision):
     from neural_polar_decoder_amd import reference_polar_code
     d = trained_fixture(NAME)
-    net = net_from(d)
+    net = net_from(d, precision)
     N, K = int(d["N"]), int(d["K"])
     code = reference_polar_code(N, K)
     assert np.array_equal(np.asarray(code.info_positions), d["info"])

@@ -7,6 +7,8 @@ B=$1; shift
 mkdir -p gpurun_out/train
 for c in "$@"; do
   [ -f train_state/$c.pt ] && cp train_state/$c.pt gpurun_out/train/$c.pt
+  INIT=""
+  [ -f train_state/$c.init.pt ] && INIT="--init train_state/$c.init.pt"
   timeout -k 10 $((B + 120)) python -u tests/golden/train_crisp_gpu.py $c --state gpurun_out/train/$c.pt \
-      --out gpurun_out/train/$c.net.pt --budget-s $B 2>&1 | tee -a gpurun_out/train/$c.log
+      --out gpurun_out/train/$c.net.pt --budget-s $B $INIT 2>&1 | tee -a gpurun_out/train/$c.log
 done
