@@ -625,9 +625,22 @@ def conv_leg(dev, rank, world, timer, batch=8192):
     ms = event_ms(lambda: net.logits(y), 2, stream)
     flop_cw = 258.8e6  # 2 x (95.5 M conv + 33.9 M FC) MAC
     tf = flop_cw * batch / (ms / 1e3) / 1e12
+    # the same forward with the conv layers on the fp16x3 split (FC layers fp32), and its logits against fp32's
+    net.precision = "fp16x3"
+    t16 = timer(lambda: net.logits(y), iters=3, warm=1)
+    ms16 = event_ms(lambda: net.logits(y), 2, stream)
+    l16, _ = net.logits(y[:512])
+    net.precision = "fp32"
+    l32, _ = net.logits(y[:512])
     return {"value": world * batch / t, "unit": "codewords/s", "batch_per_gpu": batch, "avg_forward_ms": ms,
             "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
             "frac": tf / FP32_PEAK_TF, "config": "configs[4]: Polar(256,128) convNet embed 128, fp32, seeded weights",
+            "fp16x3_conv_layers": {"value": world * batch / t16, "avg_forward_ms": ms16,
+                                   "achieved_tflops": flop_cw * batch / (ms16 / 1e3) / 1e12,
+                                   "max_abs_logit_diff_vs_fp32": float((l16 - l32).abs().max()),
+                                   "note": "conv layers (cin > 1) on v_mfma_f32_32x32x16_f16, hi + lo split; FC and "
+                                           "LayerNorm fp32; error vs float64 held to the fp32 path's by "
+                                           "tests/test_conv_gpu.py"},
             "trained_scaled_down": trained_conv_curve(dev, rank, world)}
 
 
