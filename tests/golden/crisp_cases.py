@@ -25,10 +25,16 @@ CASES = {
     "trained_crisp_32_16": dict(_COMMON, code="Polar", profile="rev_polar", N=32, K=16, seed_init=3216,
                                 curriculum=_cur(4, 2000, 16, 1000, 0, 8000, who="ref"), ref_lr=1e-3,
                                 n_logit=512, n_sc=1 << 17, seed_dec=31, seed_mc=37),
-    # K = 8 .. 32 on the GPU, then the reference's loop at K = 32
-    "trained_crisp_64_32": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6432,
-                                curriculum=_cur(8, 5000, 32, 2000, 30000, 1000), ref_lr=2e-4,
+    # K = 8 .. 32 on the GPU, easiest bits first (rate profile 'polar', run_rnn_e2h.sh's direction), then the
+    # reference's loop at K = 32.  (The hard-first order of run_crisp.sh, kept below as trained_crisp_64_32_h2e, left
+    # the hidden-64 net at BER 0.33-0.42 / BLER ~1 over 0-4 dB after 81k GPU steps: the 24 more reliable bits added
+    # after K = 8 stayed near coin flips, 0.5 error on bits 38-58 even at 10 dB.)
+    "trained_crisp_64_32": dict(_COMMON, code="Polar", profile="polar", N=64, K=32, seed_init=6433,
+                                curriculum=_cur(8, 3000, 32, 1000, 10000, 1000), ref_lr=2e-4,
                                 n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
+    "trained_crisp_64_32_h2e": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6432,
+                                    curriculum=_cur(8, 5000, 32, 2000, 30000, 1000), ref_lr=2e-4,
+                                    n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
     # PAC(128,64) 'RM' (configs[3], rnn_all.py:61 --code PAC): K = 8 .. 64 on the GPU, then the reference's loop
     "trained_pac_128_64": dict(_COMMON, code="PAC", profile="rev_RM", N=128, K=64, seed_init=12864,
                                curriculum=_cur(8, 5000, 64, 800, 20000, 400), ref_lr=2e-4,
