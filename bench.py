@@ -638,9 +638,9 @@ def conv_leg(dev, rank, world, timer, batch=8192):
             "fp16x3_conv_layers": {"value": world * batch / t16, "avg_forward_ms": ms16,
                                    "achieved_tflops": flop_cw * batch / (ms16 / 1e3) / 1e12,
                                    "max_abs_logit_diff_vs_fp32": float((l16 - l32).abs().max()),
-                                   "note": "conv layers (cin > 1) on v_mfma_f32_32x32x16_f16, hi + lo split; FC and "
-                                           "LayerNorm fp32; error vs float64 held to the fp32 path's by "
-                                           "tests/test_conv_gpu.py"},
+                                   "note": "conv layers (cin > 1) and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo "
+                                           "split; layer 0, epilogues and LayerNorm fp32; error vs float64 held to "
+                                           "the fp32 path's by tests/test_conv_gpu.py"},
             "trained_scaled_down": trained_conv_curve(dev, rank, world)}
 
 

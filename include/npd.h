@@ -241,9 +241,9 @@ int npd_gru_decode(const npd_gru* gru, const float* y, const uint8_t* is_info, i
  * convNet (models.py:691-772) forward/decode.  weights: host fp32 in state_dict order
  * (layers1.0.weight, layers1.0.bias, ..., layersFin.4.bias, layer_norm.weight, layer_norm.bias).
  * embed = config.embed_dim (even), N = config.N = config.max_len.
- * precision: 0 = fp32 (exact fp32 FMA chains); 3 = fp16x3 conv layers (cin > 1: hi + lo fp16 operands on the fp16
- * MFMA, three products per multiply, fp32 accumulation, weights scaled by 2^SW per layer and activations by 2^4
- * before the split; FC layers and LayerNorm fp32).
+ * precision: 0 = fp32 (exact fp32 FMA chains); 3 = fp16x3 (conv layers with cin > 1 and the Linear layers: hi + lo
+ * fp16 operands on the fp16 MFMA, three products per multiply, fp32 accumulation, weights scaled by 2^SW per layer
+ * and activations by 2^4 before the split; layer 0, epilogues and LayerNorm fp32).
  */
 int npd_conv_create(int N, int embed, const float* weights, int64_t n_weights, int precision, npd_conv** out);
 int npd_conv_destroy(npd_conv* conv);

@@ -327,6 +327,94 @@ __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, co
     }
 }
 
+// ------------------------------------------------------------------------------ FC GEMM, fp16x3
+// precision 3: the same 64 x 64 block tile on v_mfma_f32_32x32x16_f16, hi + lo fp16 operands, three products per
+// multiply, fp32 accumulation.  X (activations, fp32) is split as it is staged (x 2^SA); W arrives pre-split on the
+// host (hi and lo planes of fp16(w 2^SW), same row-major (Nout, K) layout).  LDS: per buffer four fp16 planes (A hi,
+// A lo, B hi, B lo) of 64 rows x 32 k, row stride 40 (16-B aligned, conflict-free row reads); k-step s of a 32-wide K
+// block reads k = 16 s + 8 h .. + 7 (one ds_read_b128 per plane).  6 MFMAs of 32 cycles per K block per wave against
+// 16 fp32 MFMAs of 64.  Epilogue: descale 2^-(SW+SA) (exact), bias, GELU.
+constexpr int GS16 = GK + 8;
+
+__global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Whi,
+                                                       const uint16_t* __restrict__ Wlo, const float* __restrict__ bias,
+                                                       float* __restrict__ out, int M, int K, int Nout, int act,
+                                                       float descale) {
+    __shared__ __attribute__((aligned(16))) _Float16 sm[2][4][64 * GS16];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int m0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+    const int msub = wave & 1, jsub = wave >> 1;
+    // loader: A 64 rows x 32 k fp32 = 512 f4 (2 per thread); B planes 64 x 32 fp16 = 256 x 16 B (1 per thread each)
+    f4 ra[2];
+    f4 rbh, rbl;
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            int mr = m0 + r;
+            if (mr >= M) mr = M - 1;
+            ra[u] = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
+        }
+        const int r = tid >> 2, c8 = (tid & 3) * 8;
+        rbh = *reinterpret_cast<const f4*>(Whi + (int64_t)(j0 + r) * K + k0 + c8);
+        rbl = *reinterpret_cast<const f4*>(Wlo + (int64_t)(j0 + r) * K + k0 + c8);
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            hf4 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = ra[u][e] * (float)(1 << kSplitSA);
+                hi[e] = (_Float16)x;
+                lo[e] = (_Float16)(x - (float)hi[e]);
+            }
+            *reinterpret_cast<hf4*>(&sm[buf][0][r * GS16 + c4]) = hi;
+            *reinterpret_cast<hf4*>(&sm[buf][1][r * GS16 + c4]) = lo;
+        }
+        const int r = tid >> 2, c8 = (tid & 3) * 8;
+        *reinterpret_cast<f4*>(&sm[buf][2][r * GS16 + c8]) = rbh;
+        *reinterpret_cast<f4*>(&sm[buf][3][r * GS16 + c8]) = rbl;
+    };
+    f16v acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nk = K / GK;
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    const int ar = (msub * 32 + col) * GS16 + 8 * h, br = (jsub * 32 + col) * GS16 + 8 * h;
+    for (int kb = 0; kb < nk; ++kb) {
+        const int cur = kb & 1;
+        if (kb + 1 < nk) fetch((kb + 1) * GK);
+#pragma unroll
+        for (int st = 0; st < GK / 16; ++st) {
+            const hf8 ah = *reinterpret_cast<const hf8*>(&sm[cur][0][ar + 16 * st]);
+            const hf8 al = *reinterpret_cast<const hf8*>(&sm[cur][1][ar + 16 * st]);
+            const hf8 bh = *reinterpret_cast<const hf8*>(&sm[cur][2][br + 16 * st]);
+            const hf8 bl = *reinterpret_cast<const hf8*>(&sm[cur][3][br + 16 * st]);
+            acc = mfma16(ah, bh, acc);
+            acc = mfma16(ah, bl, acc);
+            acc = mfma16(al, bh, acc);
+        }
+        if (kb + 1 < nk) stash(cur ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + msub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int j = j0 + jsub * 32 + col;
+        if (m < M) {
+            float v = fmaf(acc[r], descale, bias[j]);
+            if (act) v = gelu(v);
+            out[(int64_t)m * Nout + j] = v;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------ LayerNorm + sign
 __global__ __launch_bounds__(256) void layernorm_sign_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                              const float* __restrict__ be, float* __restrict__ logits,
@@ -367,6 +455,8 @@ struct npd_conv {
     float* img;         // device: permuted conv weights + biases + FC weights/biases + LN params
     int64_t off_fc[3][2];  // (weight, bias) offsets of the three Linear layers
     int64_t off_ln[2];
+    int64_t off_fc16[3][2];  // precision 3: (hi, lo) fp16 weight planes of the Linear layers (offsets in floats)
+    float fc_descale[3];
 };
 
 static void conv_spec(int E, int idx, int& cin, int& cout, int& dil, int& res) {
@@ -488,6 +578,29 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
                     for (int l = 0; l < N; ++l) img[base + j * fcin[0] + (int64_t)l * E + cc] = p[j * fcin[0] + (int64_t)cc * N + l];
         } else {
             img.insert(img.end(), p, p + fcin[f] * fcout[f]);
+        }
+        if (precision == 3) {
+            // hi / lo fp16 planes of the (permuted) weights x 2^SW, max |w| 2^SW in [2^12, 2^13)
+            const int64_t nwf = fcin[f] * fcout[f];
+            const int64_t wsrc = c->off_fc[f][0];
+            float m = 0.0f;
+            for (int64_t i = 0; i < nwf; ++i) m = fmaxf(m, fabsf(img[wsrc + i]));
+            const int sw = m > 0.0f ? 12 - (int)floorf(log2f(m)) : 0;
+            const float sc = ldexpf(1.0f, sw);
+            c->fc_descale[f] = ldexpf(1.0f, -(sw + kSplitSA));
+            while (img.size() % 4) img.push_back(0.0f);
+            c->off_fc16[f][0] = (int64_t)img.size();
+            c->off_fc16[f][1] = c->off_fc16[f][0] + (nwf + 7) / 8 * 4;  // 16-B aligned lo plane
+            img.resize(c->off_fc16[f][1] + (nwf + 7) / 8 * 4, 0.0f);
+            uint16_t* hp = reinterpret_cast<uint16_t*>(img.data() + c->off_fc16[f][0]);
+            uint16_t* lp = reinterpret_cast<uint16_t*>(img.data() + c->off_fc16[f][1]);
+            for (int64_t i = 0; i < nwf; ++i) {
+                const float v = img[wsrc + i] * sc;
+                const _Float16 hi = (_Float16)v;
+                const _Float16 lo = (_Float16)(v - (float)hi);
+                memcpy(hp + i, &hi, 2);
+                memcpy(lp + i, &lo, 2);
+            }
         }
         p += fcin[f] * fcout[f];
         c->off_fc[f][1] = (int64_t)img.size();
@@ -645,15 +758,23 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
         const float* flat = bufs[in_idx];  // (nb, N*E): l*E + c (FC0's weights are permuted to match)
         const int64_t K1 = (int64_t)E * N;
         dim3 g1(4 * N / 64, (unsigned)((nb + 63) / 64));
-        hipLaunchKernelGGL(fc_kernel, g1, dim3(256), 0, s, flat, c->img + c->off_fc[0][0], c->img + c->off_fc[0][1], H1,
-                           (int)nb, (int)K1, 4 * N, 1);
-        int rc = launch_check("fc_kernel launch");
-        if (rc) return rc;
         dim3 g2(N / 64, (unsigned)((nb + 63) / 64));
-        hipLaunchKernelGGL(fc_kernel, g2, dim3(256), 0, s, H1, c->img + c->off_fc[1][0], c->img + c->off_fc[1][1], H2,
-                           (int)nb, 4 * N, N, 1);
-        hipLaunchKernelGGL(fc_kernel, g2, dim3(256), 0, s, H2, c->img + c->off_fc[2][0], c->img + c->off_fc[2][1], H3,
-                           (int)nb, N, N, 0);
+        const float* fin[3] = {flat, H1, H2};
+        float* fout[3] = {H1, H2, H3};
+        const int fk[3] = {(int)K1, 4 * N, N}, fo[3] = {4 * N, N, N}, fa[3] = {1, 1, 0};
+        for (int f = 0; f < 3; ++f) {
+            if (c->precision == 3) {
+                const uint16_t* wh = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][0]);
+                const uint16_t* wl = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][1]);
+                hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
+                                   c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_descale[f]);
+            } else {
+                hipLaunchKernelGGL(fc_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], c->img + c->off_fc[f][0],
+                                   c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f]);
+            }
+        }
+        int rc = launch_check("fc launch");
+        if (rc) return rc;
         hipLaunchKernelGGL(layernorm_sign_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, H3,
                            c->img + c->off_ln[0], c->img + c->off_ln[1], logits ? logits + b0 * N : nullptr,
                            decoded ? decoded + b0 * N : nullptr, (int)nb, N);

@@ -18,8 +18,9 @@ from . import _lib
 
 class convNet(nn.Module):
     """models.convNet.  ``precision`` (keyword, not in the reference): "fp32" (default; exact fp32 FMA chains on
-    v_mfma_f32_32x32x2_f32) or "fp16x3" (the conv layers with cin > 1 on v_mfma_f32_32x32x16_f16 with hi + lo fp16
-    operands, three products per multiply, fp32 accumulation; FC layers and LayerNorm stay fp32)."""
+    v_mfma_f32_32x32x2_f32) or "fp16x3" (the conv layers with cin > 1 and the three Linear layers on v_mfma_f32_32x32x16_f16
+    with hi + lo fp16 operands, three products per multiply, fp32 accumulation; layer 0, GELU, residuals and
+    LayerNorm stay fp32)."""
 
     PRECISIONS = {"fp32": 0, "fp16x3": 3}
 

@@ -93,8 +93,8 @@ def test_conv_forward_returns_input4(oracle):
 # ------------------------------------------------------------------------------------------- fp16x3 conv layers
 @pytest.mark.parametrize("name", ["conv_small_64", "conv_c5_256"])
 def test_conv_fp16x3_golden(name):
-    """precision "fp16x3" (conv layers with cin > 1 on the fp16 MFMA, hi + lo split, 3 products per multiply, fp32
-    accumulation) held to the fp32 path's bars on the reference's golden logits: within 1e-5, decisions identical
+    """precision "fp16x3" (conv layers with cin > 1 and the Linear layers on the fp16 MFMA, hi + lo split, 3 products
+    per multiply, fp32 accumulation) held to the fp32 path's bars on the reference's golden logits: within 1e-5, decisions identical
     wherever the reference logit is farther than 1e-5 from zero (embed 16: 8-channel layers padded to 16; C5: embed
     128, N 256, 4 position tiles per wave)."""
     d = golden(f"{name}.npz")
