@@ -26,6 +26,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 LOGIT_ATOL = 2e-5
 CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64"]
+# fixtures whose reference BLER curve falls inside the dB bar's domain ([1e-3, 0.9]) at two or more SNR points; the
+# hidden-64 Polar(64,32) net never learned to decode (BLER ~ 1 over 0-4 dB): z-tests only
+DB_CASES = {"trained_crisp_32_16", "trained_pac_128_64"}
 
 
 def build(d, precision="fp32"):
@@ -119,4 +122,5 @@ def test_trained_gru_ber_curve_matches_reference(name):
         if 1e-3 <= pr <= 0.9:
             assert o is not None and abs(o) <= 0.05, (s, o, pr)
             checked += 1
-    assert checked >= 2, f"only {checked} SNR points with reference BLER in [1e-3, 0.9]: the dB bar cannot run"
+    if name in DB_CASES:
+        assert checked >= 2, f"only {checked} SNR points with reference BLER in [1e-3, 0.9]: the dB bar cannot run"
