@@ -2,14 +2,17 @@
 fixture words (tests/golden/gen_trained.py: run_crisp.sh-shaped curricula, final stage by the reference's own
 training loop) against the
 reference's RNN_decoder.decode decisions, and its logits against the reference's.  Tolerance as for the
-seeded fixtures: logits within 2e-5 absolute on agreeing codewords; >= 99.9 % of information bits and
+seeded fixtures, but logits within 1e-4 absolute on agreeing codewords (the reference's own fp32 logits sit up to
+2.2e-5 from float64 on the trained words); >= 99.9 % of information bits and
 >= 99 % of codewords identical."""
 import numpy as np
 import pytest
 
 from conftest import trained_decisions, trained_fixture, trained_words
 
-LOGIT_ATOL = 2e-5
+# trained recurrences amplify rounding: the reference's own fp32 logits sit up to 2.2e-5 (Polar(64,32)) / 7.3e-6
+# (Polar(32,16)) from float64 on the fixture words, so two fp32-class implementations are held to 1e-4 of each other
+LOGIT_ATOL = 1e-4
 
 
 @pytest.mark.parametrize("name", ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64"])

@@ -8,8 +8,8 @@ per SNR through RNN_decoder.decode on the CPU), by tests/golden/gen_trained.py.
 
 Stated tolerance for the neural path (the north_star's "within a stated BER tolerance"):
   (a) decisions on the fixture words: >= 99.9 % of information bits and >= 99 % of codewords identical to
-      the reference's; logits within 2e-5 absolute on codewords whose decisions agree (fp32, different
-      summation order);
+      the reference's; logits within 1e-4 absolute on codewords whose decisions agree (fp32, different
+      summation order; the reference's own logits are up to 2.2e-5 from float64 on these words);
   (b) Monte-Carlo at 2^20 words per SNR (Philox words, independent of the reference's torch draws): BLER and
       BER within 4 two-sample standard errors of the reference's curve (BLER binomial; BER with the
       per-codeword bit-error variance from both sides), and the BLER curve's horizontal offset from the
@@ -24,7 +24,9 @@ from conftest import db_offsets, trained_decisions, trained_fixture, trained_wor
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-LOGIT_ATOL = 2e-5
+# trained recurrences amplify rounding: the reference's own fp32 logits sit up to 2.2e-5 (Polar(64,32)) / 7.3e-6
+# (Polar(32,16)) from float64 on the fixture words, so two fp32-class implementations are held to 1e-4 of each other
+LOGIT_ATOL = 1e-4
 CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64"]
 # fixtures whose reference BLER curve falls inside the dB bar's domain ([1e-3, 0.9]) at two or more SNR points; the
 # hidden-64 Polar(64,32) net never learned to decode (BLER ~ 1 over 0-4 dB): z-tests only
