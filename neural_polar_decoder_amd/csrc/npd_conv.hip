@@ -694,8 +694,6 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
-        NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    163840));
         attr = true;
     }
     for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -722,17 +720,17 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res);
             else if (c->precision == 3) {
-                // positions per block 64 P: the largest P in {4, 2, 1} with 64 P <= N whose two fp16 slab planes fit
+                // positions per block 64 P: P = 2 where 128 <= N and the two fp16 slab planes fit, else 1.  (P = 4 reuses
+                // each weight fragment over 4 position tiles but its 80 KB slab leaves one block per CU, no overlap of
+                // one block's staging with another's MFMAs: configs[4] forward 11.6-12.1 ms at P = 4, 10.3-10.6 at
+                // P = 2, 10.6-10.7 at P = 1 per 8192 codewords, profiles/round4/conv_p_ab.txt)
                 const int cs = ((L.cin + 15) & ~15) + 8;
-                int P = 4;
+                int P = 2;
                 while (P > 1 && (64 * P > N || (size_t)2 * (64 * P + 2 * halo) * cs * 2 > 160 * 1024)) P >>= 1;
                 const size_t ls = (size_t)2 * (64 * P + 2 * halo) * cs * 2;
                 dim3 gs((N + 64 * P - 1) / (64 * P), (L.cout + 63) / 64, (unsigned)nb);
                 const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff);
-                if (P == 4)
-                    hipLaunchKernelGGL(conv_layer_split_kernel<4>, gs, dim3(256), ls, s, in, o, rsrc, wi, c->img + L.boff,
-                                       L.cin, L.cout, N, L.dil, L.res, L.descale);
-                else if (P == 2)
+                if (P == 2)
                     hipLaunchKernelGGL(conv_layer_split_kernel<2>, gs, dim3(256), ls, s, in, o, rsrc, wi, c->img + L.boff,
                                        L.cin, L.cout, N, L.dil, L.res, L.descale);
                 else
