@@ -80,7 +80,8 @@ def gru_flop_per_cw(N, F):
 
 
 TRAINED_64_32 = os.path.join(ROOT, "tests", "golden", "trained_crisp_64_32.npz")
-TRAINED_PAC = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64.npz")
+TRAINED_PAC = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64.npz")  # hidden 64 (not learnable: DESIGN 2b)
+TRAINED_PAC_F512 = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64_f512.npz")
 
 
 def trained_or_seeded(code, path, info, dev, precision="fp32"):
@@ -561,9 +562,43 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
                           "bler": {str(s): float(cc[i, 1]) / n for i, s in enumerate(snrs)},
                           "weights": wdesc,
                           "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, 64),
+                          "trained_f512": pac_gru_f512(code, dev, rank, world, snrs, timer),
                           "config": "configs[3]: PAC(128,64) CRISP GRU hidden 64, 2 layers, fp32; 2^20 per SNR per GPU "
                                     "(2^23 at 8 GPUs), 0-4 dB, RCCL counter all-reduce"}
     return out
+
+
+def pac_gru_f512(code, dev, rank, world, snrs, timer, B=1 << 16):
+    """configs[3] with the net that decodes: the PAC(128,64) CRISP GRU at run_crisp.sh's width (hidden 512, 2 layers)
+    trained over the K + 1 curriculum (tests/golden/gen_trained.py, trained_pac_128_64_f512), fp32 gru_wide_kernel:
+    B words per SNR per GPU on Philox words, BER/BLER after the RCCL counter reduce, against the reference's own
+    Monte-Carlo curve for the same weights."""
+    if not os.path.exists(TRAINED_PAC_F512):
+        return None
+    net, dec, wdesc, fix = trained_or_seeded(code, TRAINED_PAC_F512, code.B, dev)
+    c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    words = []
+    for si, s_ in enumerate(snrs):
+        msg, _, y = code.mc_generate(B, s_, SEED + 512, si, rank * B, device=dev)
+        words.append((msg, y))
+
+    def step():
+        for si in range(len(snrs)):
+            count_errors(words[si][0], dec.decode(net, False, words[si][1]), c[si], cols=code.B)
+
+    dec.decode(net, False, words[0][1][:64])
+    t = timer(step, iters=1, warm=0)
+    allreduce(c, _sum(), world)
+    cc = c.cpu().numpy()
+    n = world * B
+    flop_cw = gru_flop_per_cw(128, 512)
+    return {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3, "words_per_snr": n,
+            "achieved_tflops": flop_cw * len(snrs) * B / t / 1e12, "weights": wdesc,
+            "ber": {str(s_): float(cc[i, 0]) / (n * 64) for i, s_ in enumerate(snrs)},
+            "bler": {str(s_): float(cc[i, 1]) / n for i, s_ in enumerate(snrs)},
+            "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, 64),
+            "config": "PAC(128,64) CRISP GRU hidden 512 (run_crisp.sh width), 2 layers, fp32 gru_wide_kernel, "
+                      f"{B} words per SNR per GPU, 0-4 dB"}
 
 
 def scl_leg(code64, dev, y64, snr, world, timer):

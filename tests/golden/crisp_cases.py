@@ -21,10 +21,12 @@ _COMMON = dict(F=64, layers=2, snr_train=0.0, batch=4096, lr=1e-3, lr_decay=2000
                eval_snrs=[0.0, 2.0, 4.0], n_dec=4096, n_mc=1 << 20)
 
 CASES = {
-    # entirely the reference's own loop (CPU): K = 4 .. 16
+    # the reference's own loop (CPU) for K = 4 .. 16, then a long K = 16 stage on the GPU and a last stage of the
+    # reference's loop (run_crisp.sh's final stage is 100k steps)
     "trained_crisp_32_16": dict(_COMMON, code="Polar", profile="rev_polar", N=32, K=16, seed_init=3216,
-                                curriculum=_cur(4, 2000, 16, 1000, 0, 8000, who="ref"), ref_lr=1e-3,
-                                n_logit=512, n_sc=1 << 17, seed_dec=31, seed_mc=37),
+                                curriculum=_cur(4, 2000, 16, 1000, 0, 8000, who="ref") + [(16, 40000, "gpu"),
+                                                                                         (16, 1000, "ref")],
+                                ref_lr=1e-3, n_logit=512, n_sc=1 << 17, seed_dec=31, seed_mc=37),
     # K = 8 .. 32 on the GPU, easiest bits first (rate profile 'polar', run_rnn_e2h.sh's direction), then the
     # reference's loop at K = 32.  (The hard-first order of run_crisp.sh, kept below as trained_crisp_64_32_h2e, left
     # the hidden-64 net at BER 0.33-0.42 / BLER ~1 over 0-4 dB after 81k GPU steps: the 24 more reliable bits added
@@ -35,13 +37,11 @@ CASES = {
     "trained_crisp_64_32_h2e": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6432,
                                     curriculum=_cur(8, 5000, 32, 2000, 30000, 1000), ref_lr=2e-4,
                                     n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
-    # PAC(128,64) 'RM' (configs[3], rnn_all.py:61 --code PAC): K = 8 .. 64 on the GPU, then the reference's loop
-    "trained_pac_128_64": dict(_COMMON, code="PAC", profile="rev_RM", N=128, K=64, seed_init=12864,
-                               curriculum=_cur(8, 5000, 64, 800, 20000, 400), ref_lr=2e-4,
-                               n_logit=256, n_sc=1 << 13, seed_dec=47, seed_mc=53),
-    # the same code on the easy-to-hard order (rate profile 'RM': stage K = the K highest-weight rows, run_rnn_e2h.sh's
-    # direction): the hard-first curriculum above stalls on PAC (BER 0.08-0.26 per bit even at 10 dB at K = 12)
-    "trained_pac_128_64_e2h": dict(_COMMON, code="PAC", profile="RM", N=128, K=64, seed_init=12865,
-                                   curriculum=_cur(8, 3000, 64, 800, 20000, 400), ref_lr=2e-4,
-                                   n_logit=256, n_sc=1 << 13, seed_dec=47, seed_mc=53),
+    # PAC(128,64) (configs[3], rnn_all.py:61 --code PAC, rate profile 'RM' reversed = hard first) at the CRISP script's
+    # own width (run_crisp.sh: --rnn_feature_size 512): K = 8 .. 64 on the GPU, then the reference's loop.  At hidden 64
+    # the same curriculum stalled (per-bit BER 0.08-0.26 even at 10 dB by K = 12, in either bit order).
+    # F = 512 decodes on the fp32 gru_wide_kernel
+    "trained_pac_128_64_f512": dict(_COMMON, code="PAC", profile="rev_RM", N=128, K=64, F=512, seed_init=12866,
+                                    curriculum=_cur(8, 2000, 64, 400, 10000, 20), ref_lr=2e-4,
+                                    n_logit=64, n_sc=1 << 13, n_dec=4096, n_mc=1 << 16, seed_dec=47, seed_mc=53),
 }

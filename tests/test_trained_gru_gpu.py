@@ -27,10 +27,10 @@ DEV = "cuda:0"
 # trained recurrences amplify rounding: the reference's own fp32 logits sit up to 2.2e-5 (Polar(64,32)) / 7.3e-6
 # (Polar(32,16)) from float64 on the fixture words, so two fp32-class implementations are held to 1e-4 of each other
 LOGIT_ATOL = 1e-4
-CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64"]
+CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_pac_128_64_f512"]
 # fixtures whose reference BLER curve falls inside the dB bar's domain ([1e-3, 0.9]) at two or more SNR points; the
 # hidden-64 Polar(64,32) net never learned to decode (BLER ~ 1 over 0-4 dB): z-tests only
-DB_CASES = {"trained_crisp_32_16", "trained_pac_128_64"}
+DB_CASES = {"trained_crisp_32_16", "trained_pac_128_64_f512"}
 
 
 def build(d, precision="fp32"):
@@ -44,8 +44,10 @@ def build(d, precision="fp32"):
 @pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
 @pytest.mark.parametrize("name", CASES)
 def test_trained_gru_decisions_match_reference(name, precision):
-    """fp32: the reference's arithmetic; fp16x3: the split fp16 path, held to the same bars."""
+    """fp32: the reference's arithmetic; fp16x3: the split fp16 path, held to the same bars (hidden <= 64)."""
     d = trained_fixture(name)
+    if precision != "fp32" and int(d["F"]) > 64:
+        pytest.skip("the split paths cover hidden <= 64; hidden 512 decodes on the fp32 gru_wide_kernel")
     net, dec = build(d, precision)
     info = d["info"]
     for si in range(len(d["snr"])):
@@ -119,10 +121,22 @@ def test_trained_gru_ber_curve_matches_reference(name):
     ref_bler = [int(x) / nr for x in d["mc_blk_err"]]
     offs = db_offsets(snrs, bler, snrs, ref_bler, min_bler=1e-3)
     checked = 0
-    for s, o, pr in zip(snrs, offs, ref_bler):
-        # the dB offset is resolvable where the reference's curve falls: BLER in [1e-3, 0.9]
-        if 1e-3 <= pr <= 0.9:
-            assert o is not None and abs(o) <= 0.05, (s, o, pr)
+    lr = np.log(np.maximum(ref_bler, 1e-300))
+    for i, (s, o, p, pr) in enumerate(zip(snrs, offs, bler, ref_bler)):
+        # the dB offset is defined where the reference's curve falls (BLER in [1e-3, 0.9]) and resolvable where the
+        # two Monte-Carlo samples pin it: 3 sigma_dB <= 0.05, sigma_dB = the binomial sigma of ln BLER of both
+        # curves over the reference's local slope |d ln BLER / d SNR|; there the +-0.05 dB bar holds, elsewhere in
+        # the domain the offset must stay within its own 3 sigma
+        if not 1e-3 <= pr <= 0.9:
+            continue
+        j0, j1 = max(i - 1, 0), min(i + 1, len(snrs) - 1)
+        slope = abs(lr[j1] - lr[j0]) / (snrs[j1] - snrs[j0])
+        sig = np.sqrt((1 - p) / (p * n) + (1 - pr) / (pr * nr)) / max(slope, 1e-9)
+        assert o is not None, (s, p, pr)
+        if 3 * sig <= 0.05:
+            assert abs(o) <= 0.05, (s, o, pr, sig)
             checked += 1
+        else:
+            assert abs(o) <= 3 * sig, (s, o, pr, sig)
     if name in DB_CASES:
-        assert checked >= 2, f"only {checked} SNR points with reference BLER in [1e-3, 0.9]: the dB bar cannot run"
+        assert checked >= 2, f"only {checked} SNR points where the +-0.05 dB bar is defined and resolvable"
