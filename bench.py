@@ -18,7 +18,7 @@ between barriers and reports the max over ranks; whole-job codewords/s):
   pac_gru         configs[3]: PAC(128,64) CRISP GRU, 2^20 codewords per GPU (2^23 at 8 GPUs), RCCL
                   all-reduce of the BER/BLER counters
   pac_sc          PAC(128,64) SC decoding (the configs[3] eval's SC baseline, rnn_all.py:696)
-  conv_model      configs[4]: Polar(256,128) convNet (embed 128), fp32 MFMA
+  conv_model      configs[4]: Polar(256,128) convNet (embed 128), fp16x3 split MFMA (fp32 MFMA path beside)
   scl             SC-List L = 4, 8 at Polar(64,32) and L = 4 at Polar(256,128) (run_models.py:329)
   sc_lse          exact-LSE SC (polar.py:209-279)
 
@@ -51,6 +51,7 @@ N_CODE, K_CODE = 64, 32
 BYTES_PER_CW = 4 * N_CODE + 4 * K_CODE  # y in + msg_hat out
 HBM_PEAK_GBS = 8000.0                    # MI355X spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy
 FP32_PEAK_TF = 157.3                     # MI355X fp32 vector / fp32 MFMA (MI355X_MICROARCH.md)
+FP16_PEAK_TF = 2516.6                    # MI355X dense fp16 / bf16 MFMA (MI355X_MICROARCH.md)
 SEED = 1234
 # the reference's own sc_decode_new curve (tests/golden/sc_anchors_64_32.npz: 2e5 words at 0-1 dB, 1e6 at 2-4 dB)
 ANCHORS_NPZ = os.path.join(ROOT, "tests", "golden", "sc_anchors_64_32.npz")
@@ -80,8 +81,7 @@ def gru_flop_per_cw(N, F):
 
 
 TRAINED_64_32 = os.path.join(ROOT, "tests", "golden", "trained_crisp_64_32.npz")
-TRAINED_PAC = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64.npz")  # hidden 64 (not learnable: DESIGN 2b)
-TRAINED_PAC_F512 = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64_f512.npz")
+TRAINED_PAC = os.path.join(ROOT, "tests", "golden", "trained_pac_128_64.npz")  # none trained yet
 
 
 def trained_or_seeded(code, path, info, dev, precision="fp32"):
@@ -562,43 +562,9 @@ def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
                           "bler": {str(s): float(cc[i, 1]) / n for i, s in enumerate(snrs)},
                           "weights": wdesc,
                           "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, 64),
-                          "trained_f512": pac_gru_f512(code, dev, rank, world, snrs, timer),
                           "config": "configs[3]: PAC(128,64) CRISP GRU hidden 64, 2 layers, fp32; 2^20 per SNR per GPU "
                                     "(2^23 at 8 GPUs), 0-4 dB, RCCL counter all-reduce"}
     return out
-
-
-def pac_gru_f512(code, dev, rank, world, snrs, timer, B=1 << 16):
-    """configs[3] with the net that decodes: the PAC(128,64) CRISP GRU at run_crisp.sh's width (hidden 512, 2 layers)
-    trained over the K + 1 curriculum (tests/golden/gen_trained.py, trained_pac_128_64_f512), fp32 gru_wide_kernel:
-    B words per SNR per GPU on Philox words, BER/BLER after the RCCL counter reduce, against the reference's own
-    Monte-Carlo curve for the same weights."""
-    if not os.path.exists(TRAINED_PAC_F512):
-        return None
-    net, dec, wdesc, fix = trained_or_seeded(code, TRAINED_PAC_F512, code.B, dev)
-    c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
-    words = []
-    for si, s_ in enumerate(snrs):
-        msg, _, y = code.mc_generate(B, s_, SEED + 512, si, rank * B, device=dev)
-        words.append((msg, y))
-
-    def step():
-        for si in range(len(snrs)):
-            count_errors(words[si][0], dec.decode(net, False, words[si][1]), c[si], cols=code.B)
-
-    dec.decode(net, False, words[0][1][:64])
-    t = timer(step, iters=1, warm=0)
-    allreduce(c, _sum(), world)
-    cc = c.cpu().numpy()
-    n = world * B
-    flop_cw = gru_flop_per_cw(128, 512)
-    return {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_step": t * 1e3, "words_per_snr": n,
-            "achieved_tflops": flop_cw * len(snrs) * B / t / 1e12, "weights": wdesc,
-            "ber": {str(s_): float(cc[i, 0]) / (n * 64) for i, s_ in enumerate(snrs)},
-            "bler": {str(s_): float(cc[i, 1]) / n for i, s_ in enumerate(snrs)},
-            "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, 64),
-            "config": "PAC(128,64) CRISP GRU hidden 512 (run_crisp.sh width), 2 layers, fp32 gru_wide_kernel, "
-                      f"{B} words per SNR per GPU, 0-4 dB"}
 
 
 def scl_leg(code64, dev, y64, snr, world, timer):
@@ -647,35 +613,50 @@ def lse_leg(code, dev, y, snr, world, timer):
             "config": "Polar(64,32) sc_decode exact-LSE (polar.py:209-279), 2 dB, msg_hat out"}
 
 
+CONV_PRECISION_JSON = os.path.join(ROOT, "profiles", "round4", "conv_precision.json")
+
+
 def conv_leg(dev, rank, world, timer, batch=8192):
-    """configs[4]: Polar(256,128) convNet decoder, embed 128 (run_alt.sh), seeded random weights, fp32
-    MFMA kernels; batch per GPU, whole-job codewords/s."""
+    """configs[4]: Polar(256,128) convNet decoder, embed 128 (run_alt.sh), seeded random weights; batch per GPU,
+    whole-job codewords/s.  The record runs the fp16x3 path (conv and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo
+    split, fp32 accumulation): its logit error against a float64 forward is below the fp32 path's at every percentile
+    (profiles/round4/conv_precision.json, tools/conv_precision.py; enforced by tests/test_conv_gpu.py); the fp32 MFMA
+    path is reported beside it (fp32_path)."""
     from neural_polar_decoder_amd import reference_polar_code
     from neural_polar_decoder_amd.montecarlo import seeded_conv
     net = seeded_conv(256, 128, seed=0, device=dev)
     code = reference_polar_code(256, 128)
     _, _, y = code.mc_generate(batch, 1.0, SEED, 0, rank * batch, device=dev, want_msg=False)
     stream = torch.cuda.current_stream(dev)
-    t = timer(lambda: net.logits(y), iters=3, warm=1)
-    ms = event_ms(lambda: net.logits(y), 2, stream)
     flop_cw = 258.8e6  # SURVEY.md 8(d): 2 x (95.5 M conv + 33.9 M FC) MAC
-    tf = flop_cw * batch / (ms / 1e3) / 1e12
-    # the same forward with the conv layers on the fp16x3 split (FC layers fp32), and its logits against fp32's
-    net.precision = "fp16x3"
-    t16 = timer(lambda: net.logits(y), iters=3, warm=1)
-    ms16 = event_ms(lambda: net.logits(y), 2, stream)
-    l16, _ = net.logits(y[:512])
+    res = {}
+    for prec in ("fp32", "fp16x3"):
+        net.precision = prec
+        t = timer(lambda: net.logits(y), iters=3, warm=1)
+        ms = event_ms(lambda: net.logits(y), 2, stream)
+        lg, _ = net.logits(y[:512])
+        res[prec] = dict(t=t, ms=ms, lg=lg, tf=flop_cw * batch / (ms / 1e3) / 1e12)
     net.precision = "fp32"
-    l32, _ = net.logits(y[:512])
-    return {"value": world * batch / t, "unit": "codewords/s", "batch_per_gpu": batch, "avg_forward_ms": ms,
-            "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
-            "frac": tf / FP32_PEAK_TF, "config": "configs[4]: Polar(256,128) convNet embed 128, fp32, seeded weights",
-            "fp16x3_conv_layers": {"value": world * batch / t16, "avg_forward_ms": ms16,
-                                   "achieved_tflops": flop_cw * batch / (ms16 / 1e3) / 1e12,
-                                   "max_abs_logit_diff_vs_fp32": float((l16 - l32).abs().max()),
-                                   "note": "conv layers (cin > 1) and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo "
-                                           "split; layer 0, epilogues and LayerNorm fp32; error vs float64 held to "
-                                           "the fp32 path's by tests/test_conv_gpu.py"},
+    p16, p32 = res["fp16x3"], res["fp32"]
+    prec_table = json.load(open(CONV_PRECISION_JSON)) if os.path.exists(CONV_PRECISION_JSON) else None
+    return {"value": world * batch / p16["t"], "unit": "codewords/s", "batch_per_gpu": batch,
+            "avg_forward_ms": p16["ms"],
+            "dtype": "fp16x3: conv layers (cin > 1) and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo fp16 split, "
+                     "3 products, fp32 accumulation; layer 0, epilogues and LayerNorm fp32",
+            "achieved_tflops_fp32_equivalent": p16["tf"],
+            "roofline": {"bound": "mfma", "kernel": "conv_split_ws_kernel / fc_split_big_kernel (fp16x3)",
+                         "achieved": 3 * p16["tf"], "unit": "TFLOP/s (fp16 MFMA work issued: 3 products)",
+                         "peak": FP16_PEAK_TF, "frac": 3 * p16["tf"] / FP16_PEAK_TF},
+            "max_abs_logit_diff_vs_fp32": float((p16["lg"] - p32["lg"]).abs().max()),
+            "precision_evidence": None if prec_table is None else {
+                "source": "profiles/round4/conv_precision.json (tools/conv_precision.py)",
+                "abs_logit_error_vs_float64": {c: {k: {q: v[k][q] for q in ("p50", "p99", "p99.9", "max")}
+                                                   for k in ("reference", "fp32", "fp16x3")}
+                                               for c, v in prec_table["cases"].items()}},
+            "fp32_path": {"value": world * batch / p32["t"], "avg_forward_ms": p32["ms"],
+                          "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": p32["tf"],
+                          "peak_tflops_fp32": FP32_PEAK_TF, "frac": p32["tf"] / FP32_PEAK_TF},
+            "config": "configs[4]: Polar(256,128) convNet embed 128, seeded weights",
             "trained_scaled_down": trained_conv_curve(dev, rank, world)}
 
 

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "npd_common.hpp"
@@ -253,6 +254,177 @@ __global__ __launch_bounds__(256) void conv_layer_split_kernel(const float* __re
     }
 }
 
+// ------------------------------------------------------------------------------ conv layer, fp16x3, weight-stationary
+// The same products as conv_layer_split_kernel, reorganised so that nothing but activations streams: a persistent
+// block (one per CU) keeps its waves' weight slices in registers for the whole layer and walks (codeword, 64 Q-position
+// chunk) items.  NW waves = 2 (32 output channels each) x KS channel parts x NW / 2 / KS position parts; a wave holds
+// 32 channels x 7 taps x NG / KS 16-channel groups, hi and lo (56 NG / KS VGPRs).  NW = 8 (cin 64 / 96 / 128, KS 2 or
+// 4) keeps every wave under 256 registers, so two waves share each SIMD and one's MFMAs cover the other's LDS reads;
+// the KS channel parts of a tile hand each other their partial sums through LDS and the tile's finishing wave adds
+// them.  NW = 4, KS = 1 for cin <= 48.  The next item's slab (positions plus the dilation halo, all channels, fp32) is
+// fetched into registers before the current item's MFMAs and split into the other half of a double-buffered fp16
+// hi / lo LDS slab after them, so HBM reads overlap the matrix work and no weight fragment is re-read.  Dilation <= 4
+// (conv_spec) bounds the halo at 12.
+template <int NG, int Q, int KS, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_split_ws_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                const float* __restrict__ res,
+                                                                const f4* __restrict__ wimg,
+                                                                const float* __restrict__ bias, int cin, int cout,
+                                                                int N, int dil, int do_res, float descale, int64_t nb,
+                                                                int nslices) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 slab16[];
+    constexpr int NT = 64 * NW;
+    constexpr int PT = 64 * Q;        // positions per item (2 Q tiles of 32)
+    constexpr int C4P = 4 * NG;       // float4 channel groups per staged row (pad channels zero)
+    constexpr int CSH = 16 * NG + 8;  // fp16 row stride of the LDS slab
+    constexpr int MAXE = ((PT + 24) * C4P + NT - 1) / NT;
+    constexpr int NGW = NG / KS;      // channel groups per wave
+    constexpr int PS = NW / 2 / KS;   // position parts
+    constexpr int TPW = 2 * Q / PS;   // 32-position tiles per wave
+    static_assert(NG % KS == 0 && (NW / 2) % KS == 0 && (2 * Q) % PS == 0, "wave decomposition");
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int co_sub = wave & 1, rest = wave >> 1;
+    const int kp = rest % KS, pp = rest / KS;
+    const int g0 = kp * NGW;
+    const int halo = 3 * dil;
+    const int W = PT + 2 * halo;
+    const int plane = W * CSH;
+    const int c4n = cin >> 2;
+    const int slice = blockIdx.x % nslices;
+    const int co_t32 = slice * 2 + co_sub;
+    hf8 ah[7][NGW], al[7][NGW];
+    {
+        const f4* wq = wimg + (int64_t)co_t32 * 7 * NG * 128 + lane;
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+#pragma unroll
+            for (int g = 0; g < NGW; ++g) {
+                ah[t][g] = __builtin_bit_cast(hf8, wq[(t * NG + g0 + g) * 128]);
+                al[t][g] = __builtin_bit_cast(hf8, wq[(t * NG + g0 + g) * 128 + 64]);
+            }
+    }
+    // KS > 1: partial sums of the channel parts, [wave][tile][register][lane]
+    float* const red = reinterpret_cast<float*>(slab16 + (size_t)4 * plane);
+    const int chunks = N / PT;
+    const int64_t items = nb * chunks;
+    const int64_t stride = gridDim.x / nslices;
+    int64_t item = blockIdx.x / nslices;
+    f4 pre[MAXE];
+    auto fetch = [&](int64_t it) {
+        const int64_t b = it / chunks;
+        const int l0 = (int)(it - b * chunks) * PT;
+        const f4* inb = reinterpret_cast<const f4*>(in + b * (int64_t)N * cin);
+#pragma unroll
+        for (int e = 0; e < MAXE; ++e) {
+            const int idx = tid + NT * e;
+            const int p = idx / C4P, c4 = idx - p * C4P;
+            const int l = l0 - halo + p;
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (p < W && c4 < c4n && l >= 0 && l < N) v = inb[(int64_t)l * c4n + c4];
+            pre[e] = v;
+        }
+    };
+    auto stash = [&](int buf) {
+        _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
+#pragma unroll
+        for (int e = 0; e < MAXE; ++e) {
+            const int idx = tid + NT * e;
+            const int p = idx / C4P, c4 = idx - p * C4P;
+            if (p < W) {
+                hf4 hi, lo;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float x = pre[e][j] * (float)(1 << kSplitSA);
+                    hi[j] = (_Float16)x;
+                    lo[j] = (_Float16)(x - (float)hi[j]);
+                }
+                *reinterpret_cast<hf4*>(hiP + p * CSH + 4 * c4) = hi;
+                *reinterpret_cast<hf4*>(hiP + plane + p * CSH + 4 * c4) = lo;
+            }
+        }
+    };
+    if (item < items) {
+        fetch(item);
+        stash(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    const int tbase = pp * 32 * TPW + col;  // this lane's position column of its first tile within the item
+    for (; item < items; item += stride) {
+        const int64_t nxt = item + stride;
+        if (nxt < items) fetch(nxt);
+        const _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
+        const _Float16* const loP = hiP + plane;
+        f16v acc[TPW];
+#pragma unroll
+        for (int q = 0; q < TPW; ++q)
+            acc[q] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+#pragma unroll
+            for (int g = 0; g < NGW; ++g)
+#pragma unroll
+                for (int q = 0; q < TPW; ++q) {
+                    const int off = (tbase + 32 * q + dil * t) * CSH + 16 * (g0 + g) + 8 * h;
+                    const hf8 bh = *reinterpret_cast<const hf8*>(hiP + off);
+                    const hf8 bl = *reinterpret_cast<const hf8*>(loP + off);
+                    acc[q] = mfma16(ah[t][g], bh, acc[q]);
+                    acc[q] = mfma16(ah[t][g], bl, acc[q]);
+                    acc[q] = mfma16(al[t][g], bh, acc[q]);
+                }
+        // tile q of the (co_sub, pp) group is finished by channel part q % KS
+        if constexpr (KS > 1) {
+#pragma unroll
+            for (int q = 0; q < TPW; ++q)
+                if (q % KS != kp)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) red[((wave * TPW + q) * 16 + r) * 64 + lane] = acc[q][r];
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < TPW; ++q)
+                if (q % KS == kp)
+#pragma unroll
+                    for (int k = 1; k < KS; ++k) {
+                        const int other = co_sub + 2 * ((kp + k) % KS + KS * pp);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[q][r] += red[((other * TPW + q) * 16 + r) * 64 + lane];
+                    }
+        }
+        const int64_t b = item / chunks;
+        const int l0 = (int)(item - b * chunks) * PT;
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            if (q % KS != kp) continue;
+            const int l = l0 + tbase + 32 * q;
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int co = co_t32 * 32 + 8 * r4 + 4 * h;
+                if (co < cout) {
+                    const int64_t o = (b * N + l) * (int64_t)cout + co;
+                    const f4 bb = *reinterpret_cast<const f4*>(bias + co);
+                    f4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(acc[q][4 * r4 + e], descale, bb[e]));
+                    if (do_res) v += *reinterpret_cast<const f4*>(res + o);
+                    *reinterpret_cast<f4*>(out + o) = v;
+                }
+            }
+        }
+        if (nxt < items) stash(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
+// LDS bytes of conv_split_ws_kernel: two slab buffers (hi + lo planes) and, for KS > 1, the partial-sum exchange
+static size_t ws_lds_bytes(int ng, int Q, int ks, int nw, int dil) {
+    const size_t slabs = (size_t)2 * 2 * (64 * Q + 6 * dil) * (16 * ng + 8) * 2;
+    const int tpw = 2 * Q / (nw / 2 / ks);
+    return slabs + (ks > 1 ? (size_t)nw * tpw * 16 * 64 * 4 : 0);
+}
+
 // ------------------------------------------------------------------------------ FC GEMM
 // out[m][j] = act(sum_k X[m][k] * Wt[j][k] + bias[j]);  block tile 64 (m) x 64 (j), K step 32.
 // LDS rows of stride GK + 4 (16-B aligned; 32 rows read with ds_read_b128 at one k offset hit every bank
@@ -413,6 +585,144 @@ __global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__
             out[(int64_t)m * Nout + j] = v;
         }
     }
+}
+
+// fp16x3 FC GEMM with a 128 x 128 block tile (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from N = 128): four
+// waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA tiles, so an A fragment pair feeds two tiles and a B pair two -- 16
+// ds_read_b128 per 24 MFMAs of a 32-wide K block instead of 4 per 6 -- and each X / W element staged in LDS is read by
+// 4 tiles instead of 2.  At one workgroup per CU a K block's MFMAs (~770 cycles) are shorter than an HBM round trip,
+// so the loads run FD = 3 K blocks ahead through a register ring, split / stored into the other LDS buffer one block
+// ahead.  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2): the column tiles of one row
+// block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords -- is read from HBM once, not once per
+// column tile.  LDS 80 KB (dynamic).
+constexpr int FB = 128;
+constexpr int FD = 3;
+constexpr size_t kFcBigLds = (size_t)2 * 4 * FB * GS16 * 2;
+
+__global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Whi,
+                                                           const uint16_t* __restrict__ Wlo,
+                                                           const float* __restrict__ bias, float* __restrict__ out,
+                                                           int M, int K, int Nout, int act, float descale) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [buf][plane A hi, A lo, B hi, B lo][128][GS16]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    // XCD-aware tile order (grid = column tiles x row tiles, a multiple of 8 or dealt linearly)
+    const int gx = Nout / FB;
+    const int total = gridDim.x;
+    int lin = blockIdx.x;
+    if ((total & 7) == 0) lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
+    const int wm = wave & 1, wn = wave >> 1;
+    constexpr int PL = FB * GS16;  // halfs per plane
+    // loader: A 128 rows x 32 k fp32 = 1024 f4 (4 per thread); B planes 128 x 32 fp16 = 512 x 16 B (2 per thread each)
+    f4 ra[FD][4], rbh[FD][2], rbl[FD][2];
+    auto fetch = [&](int slot, int k0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            int mr = m0 + r;
+            if (mr >= M) mr = M - 1;
+            ra[slot][u] = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 2, c8 = (idx & 3) * 8;
+            rbh[slot][u] = *reinterpret_cast<const f4*>(Whi + (int64_t)(j0 + r) * K + k0 + c8);
+            rbl[slot][u] = *reinterpret_cast<const f4*>(Wlo + (int64_t)(j0 + r) * K + k0 + c8);
+        }
+    };
+    auto stash = [&](int slot, int buf) {
+        _Float16* const base = smb + (size_t)buf * 4 * PL;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            hf4 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = ra[slot][u][e] * (float)(1 << kSplitSA);
+                hi[e] = (_Float16)x;
+                lo[e] = (_Float16)(x - (float)hi[e]);
+            }
+            *reinterpret_cast<hf4*>(base + r * GS16 + c4) = hi;
+            *reinterpret_cast<hf4*>(base + PL + r * GS16 + c4) = lo;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = tid + 256 * u;
+            const int r = idx >> 2, c8 = (idx & 3) * 8;
+            *reinterpret_cast<f4*>(base + 2 * PL + r * GS16 + c8) = rbh[slot][u];
+            *reinterpret_cast<f4*>(base + 3 * PL + r * GS16 + c8) = rbl[slot][u];
+        }
+    };
+    f16v acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+            acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nk = K / GK;
+    const int ar = (wm * 64 + col) * GS16 + 8 * h, br = (wn * 64 + col) * GS16 + 8 * h;
+    // K block kb lives in ring slot kb % FD until it is stashed into LDS buffer kb & 1
+    fetch(0, 0);
+#pragma unroll
+    for (int d = 1; d < FD; ++d)
+        if (d < nk) fetch(d, d * GK);
+    stash(0, 0);
+    __syncthreads();
+    auto step = [&](int kb, auto slot_c) {
+        constexpr int SL = decltype(slot_c)::value;  // kb % FD
+        const _Float16* const cb = smb + (size_t)(kb & 1) * 4 * PL;
+        if (kb + FD < nk) fetch(SL, (kb + FD) * GK);  // slot SL was stashed at step kb - 1
+#pragma unroll
+        for (int st = 0; st < GK / 16; ++st) {
+            hf8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GS16 + 16 * st);
+                al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GS16 + 16 * st);
+                bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GS16 + 16 * st);
+                bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GS16 + 16 * st);
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    acc[a][b] = mfma16(ah[a], bh[b], acc[a][b]);
+                    acc[a][b] = mfma16(ah[a], bl[b], acc[a][b]);
+                    acc[a][b] = mfma16(al[a], bh[b], acc[a][b]);
+                }
+        }
+        if (kb + 1 < nk) stash((SL + 1) % FD, (kb + 1) & 1);
+        __syncthreads();
+    };
+    int kb = 0;
+    for (; kb + FD <= nk; kb += FD) {
+        step(kb, std::integral_constant<int, 0>{});
+        step(kb + 1, std::integral_constant<int, 1>{});
+        step(kb + 2, std::integral_constant<int, 2>{});
+    }
+    if (kb < nk) step(kb, std::integral_constant<int, 0>{});
+    if (kb + 1 < nk) step(kb + 1, std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int j = j0 + wn * 64 + 32 * b + col;
+            const float bj = bias[j];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 64 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < M) {
+                    float v = fmaf(acc[a][b][r], descale, bj);
+                    if (act) v = gelu(v);
+                    out[(int64_t)m * Nout + j] = v;
+                }
+            }
+        }
 }
 
 // ------------------------------------------------------------------------------ LayerNorm + sign
@@ -694,6 +1004,14 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
+        NPD_HIP(hipFuncSetAttribute((const void*)fc_split_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kFcBigLds));
+        const void* ws[9] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
+                              (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
+                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
+                              (const void*)conv_split_ws_kernel<4, 1, 2, 8>, (const void*)conv_split_ws_kernel<4, 2, 2, 8>,
+                              (const void*)conv_split_ws_kernel<8, 1, 4, 8>};
+        for (const void* k : ws) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
     }
     for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -719,7 +1037,33 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             if (L.cin == 1)
                 hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res);
-            else if (c->precision == 3) {
+            else if (c->precision == 3 && L.dil <= 4 && (L.cin <= 64 || L.cin == 128)) {
+                // weight-stationary persistent blocks: one per CU, a multiple of the 64-channel slice count.
+                // cin <= 48: 4 waves (KS 1); 64: 8 waves, 2 channel parts; 128: 8 waves, 4 channel parts, 64-position
+                // items (the 128-position slab would not fit).  Other widths (e.g. 80, 96: a 2-part split of 96 channels
+                // spills) run the slab kernel below.
+                const int ng = (L.cin + 15) / 16;
+                const int ks = ng <= 3 ? 1 : (ng == 8 ? 4 : 2);  // ng in {1, 2, 3, 4, 8}
+                const int nw = ng <= 3 ? 4 : 8;
+                const int Q = (ng <= 4 && N % 128 == 0) ? 2 : 1;
+                const int nslices = (L.cout + 63) / 64;
+                const int64_t items = nb * (N / (64 * Q)) * nslices;
+                int64_t nblk = device_cu_count();
+                nblk -= nblk % nslices;
+                if (nblk > items) nblk = items;
+                if (nblk < nslices) nblk = nslices;
+                const size_t ls = ws_lds_bytes(ng, Q, ks, nw, L.dil);
+                const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff);
+#define NPD_WS(NGV, QV, KSV, NWV)                                                                                   \
+    hipLaunchKernelGGL((conv_split_ws_kernel<NGV, QV, KSV, NWV>), dim3((unsigned)nblk), dim3(64 * NWV), ls, s, in, o, \
+                       rsrc, wi, c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, L.descale, nb, nslices)
+                if (ng == 8) NPD_WS(8, 1, 4, 8);
+                else if (ng == 4) { if (Q == 2) NPD_WS(4, 2, 2, 8); else NPD_WS(4, 1, 2, 8); }
+                else if (ng == 1) { if (Q == 2) NPD_WS(1, 2, 1, 4); else NPD_WS(1, 1, 1, 4); }
+                else if (ng == 2) { if (Q == 2) NPD_WS(2, 2, 1, 4); else NPD_WS(2, 1, 1, 4); }
+                else { if (Q == 2) NPD_WS(3, 2, 1, 4); else NPD_WS(3, 1, 1, 4); }
+#undef NPD_WS
+            } else if (c->precision == 3) {
                 // positions per block 64 P: P = 2 where 128 <= N and the two fp16 slab planes fit, else 1.  (P = 4 reuses
                 // each weight fragment over 4 position tiles but its 80 KB slab leaves one block per CU, no overlap of
                 // one block's staging with another's MFMAs: configs[4] forward 11.6-12.1 ms at P = 4, 10.3-10.6 at
@@ -764,8 +1108,14 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             if (c->precision == 3) {
                 const uint16_t* wh = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][0]);
                 const uint16_t* wl = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][1]);
-                hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
-                                   c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_descale[f]);
+                if (fo[f] % FB == 0) {
+                    dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
+                    hipLaunchKernelGGL(fc_split_big_kernel, gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,
+                                       c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_descale[f]);
+                } else {
+                    hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
+                                       c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_descale[f]);
+                }
             } else {
                 hipLaunchKernelGGL(fc_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], c->img + c->off_fc[f][0],
                                    c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f]);

@@ -136,3 +136,24 @@ def test_conv_fp16x3_error_matches_fp32_against_float64(oracle):
         print(E, N, "fp32", q32, errs["fp32"].max(), "fp16x3", q16, errs["fp16x3"].max())
         assert np.all(q16 <= 1.5 * q32), (E, N, q32, q16)
         assert errs["fp16x3"].max() <= 2.0 * errs["fp32"].max(), (E, N)
+
+
+@pytest.mark.parametrize("E,N", [(64, 128), (64, 64), (80, 64), (96, 64), (128, 256)])
+def test_conv_fp16x3_shapes_vs_oracle(oracle, E, N):
+    """The fp16x3 kernels at every shape family they dispatch on, against the float64 oracle on a ragged batch of more
+    than one 4096-codeword chunk (seeded weights, conftest.conv_weights_from_seed): embed 64 / N 128 (weight-stationary
+    conv kernel with 32-channel groups, 128-position items; the 128 x 128 FC kernel for all three Linear layers); embed
+    64 / N 64 (the 64-channel layer on 64-position items);
+    embed 80 / N 64 (40-channel layers = three 16-channel groups, 64-position items; the 80-channel layer on the
+    slab kernel; FC1 / FC2 of 64 outputs on the 64 x 64 FC kernel); embed 96 / N 64 (48-channel layers, the 96-channel
+    layer on the slab kernel); C5 (embed 128, N 256: 64-channel layers on 8 waves in 2 channel parts, the 128-channel
+    layer in 4). Same bars as the golden tests: logits within 1e-5, decisions identical away from zero."""
+    sd = conv_weights_from_seed(E, N, 100 + E)
+    net = net_from(sd, E, N, precision="fp16x3")
+    rng = np.random.default_rng(E + N)
+    B = 4096 + 37
+    y = (np.where(rng.random((B, N)) < 0.5, -1.0, 1.0) + 0.8 * rng.standard_normal((B, N))).astype(np.float32)
+    lg, dec = net.logits(torch.from_numpy(y).to(DEV))
+    sel = np.r_[0:B:97, B - 1]
+    ref = oracle.conv_forward(y[sel], sd)
+    check(lg.cpu().numpy()[sel], dec.cpu().numpy()[sel], ref)
