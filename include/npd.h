@@ -235,6 +235,25 @@ int npd_gru_destroy(npd_gru* gru);
  */
 int npd_gru_decode(const npd_gru* gru, const float* y, const uint8_t* is_info, int reverse, const float* gt,
                    float* decoded, float* logits, int64_t B, void* stream);
+/*
+ * The same decode with an initial state and an optional y input -- decoding_type 'y_h0' (rnn_all.py:523-531):
+ * hidden = net.get_h0(y), then every step's RNN input is onehot(previous decision) alone.  The handle is created
+ * from weights whose weight_ih_l0 carries N zero columns before the one-hot / sign columns (the y_input layout with
+ * the y part zero); y = NULL skips that projection.  h0: (B, F * layers) fp32 on the device, element f * layers + l =
+ * layer l, hidden unit f -- get_h0's x before its reshape(-1, F, layers).permute(2, 0, 1) (rnn_all.py:362-375).
+ * Precision 0, or the 16-codeword split kernel (F = 64, 2 layers, N % 32 == 0); y = NULL and h0 = NULL is an error.
+ */
+int npd_gru_decode_ex(const npd_gru* gru, const float* y, const float* h0, const uint8_t* is_info, int reverse,
+                      const float* gt, float* decoded, float* logits, int64_t B, void* stream);
+/*
+ * One layer of RNN_Model.get_h0 / get_Fy (rnn_all.py:362-385): out (B, Nout) = act(x (B, K) W^T + bias), W (Nout, K)
+ * row-major, all device fp32, k summed in order.  act: 0 linear, 1 relu, 2 selu, 3 elu, 4 tanh, 5 sigmoid
+ * (RNN_Model.act, rnn_all.py:346-360).  get_h0 follows layer ii with act iff ii != y_depth (rnn_all.py:364-368): every
+ * layer, the last included, when y_depth >= 2; all but the last when y_depth = 1 (two layers) -- the caller passes
+ * act = 0 for that one layer.
+ */
+int npd_ymlp_layer(const float* x, const float* W, const float* bias, float* out, int64_t B, int K, int Nout, int act,
+                   void* stream);
 
 /* ---------------------------------------------------------------------------------- conv model */
 /*

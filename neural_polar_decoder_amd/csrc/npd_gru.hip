@@ -81,7 +81,8 @@ __host__ __device__ inline int hid_of(int s, int kk) {
 struct Args {
     const float* img;
     const f4* wy;
-    const float* y;
+    const float* y;   // NULL: no y input (decoding_type 'y_h0': the RNN input is the previous bit alone)
+    const float* h0;  // NULL: zero initial state; else (B, F L), element f L + l = layer l, unit f (get_h0's x)
     const float* gt;
     float* decoded;
     float* logits;
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
         f16v P[TT];
 #pragma unroll
         for (int t = 0; t < TT; ++t) P[t] = zero;
-        {
+        if (a.y) {
             const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
             const int ng = N / 8;
             for (int s4 = 0; s4 < ng; ++s4) {
@@ -237,6 +238,17 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
         for (int t = 0; t < HT; ++t) {
             h0[t] = zero;
             h1[t] = zero;
+        }
+        if (a.h0) {  // register i of tile t = hidden unit hid_of(16 t + i, half) of codeword col
+            const float* hr = a.h0 + cwc * (int64_t)(F * L);
+#pragma unroll
+            for (int t = 0; t < HT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int f = hid_of(16 * t + i, half);
+                    h0[t][i] = hr[f * L];
+                    if constexpr (L == 2) h1[t][i] = hr[f * L + 1];
+                }
         }
         float xb = 1.0f;  // x_i: onehot index of the previous decision (or its sign); step 0: prev = +1
         const float one_or_zero = half ? 0.0f : 1.0f;
@@ -478,7 +490,8 @@ struct GeoB {
 struct ArgsB {
     const float* img;
     const f4* wy;  // [TT][N/16][64] bf16x8 fragments (hi, then lo for SPLIT 3)
-    const float* y;
+    const float* y;   // NULL: no y input (y_h0)
+    const float* h0;  // NULL: zero initial state; else (B, F L) as Args::h0 (16-codeword kernel only)
     const float* gt;
     float* decoded;
     float* logits;
@@ -998,7 +1011,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
         f4 P[G::RT];
 #pragma unroll
         for (int t = 0; t < G::RT; ++t) P[t] = c4(G::C0L0, t);
-        {
+        if (a.y) {
             const float* yr = a.y + cwc * N;
             for (int kb = 0; kb < nkb; ++kb) {
                 const f4 y0 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4);
@@ -1027,6 +1040,17 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
         for (int t = 0; t < 4; ++t) {
             h0[t] = zero;
             h1[t] = zero;
+        }
+        if (a.h0) {  // register e of tile t = hidden unit 16 t + 4 g4 + e of codeword col (F = 64, 2 layers)
+            const float* hr = a.h0 + cwc * 128;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int f = 16 * t + 4 * g4 + e;
+                    h0[t][e] = hr[2 * f];
+                    h1[t][e] = hr[2 * f + 1];
+                }
         }
         V fh[2], fl[2], gh[2], gl[2];
         split16s<SPLIT>(h0, fh, fl);
@@ -1318,9 +1342,25 @@ __global__ __launch_bounds__(64 * WideGeo<F>::NW) void gru_wide_kernel(const Arg
         const int64_t cwc = valid ? cw : a.B - 1;
         __syncthreads();  // the previous tile's last readers are done
         {
-            const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
-            for (int q = wave; q < ng; q += NW) Ys[q * 64 + lane] = yr[q];
-            for (int i = threadIdx.x; i < L * F * 8; i += NW * 64) lds4[i] = f4{0.f, 0.f, 0.f, 0.f};
+            if (a.y) {
+                const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
+                for (int q = wave; q < ng; q += NW) Ys[q * 64 + lane] = yr[q];
+            }
+            // states: f4 (4 jt + q) * 64 + lane of layer l holds units hid_of(16 jt + 4 q + e, lane >> 5), e < 4, of
+            // codeword tile * 32 + (lane & 31): zero, or the initial state a.h0 (B, F L)
+            for (int i = threadIdx.x; i < L * F * 8; i += NW * 64) {
+                f4 v = f4{0.f, 0.f, 0.f, 0.f};
+                if (a.h0) {
+                    const int l = i / (F * 8), idx = i - l * F * 8;
+                    const int ln = idx & 63, jq = idx >> 6;
+                    int64_t c = tile * 32 + (ln & 31);
+                    if (c >= a.B) c = a.B - 1;
+                    const float* hr = a.h0 + c * (int64_t)(F * L) + l;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = hr[hid_of(16 * (jq >> 2) + 4 * (jq & 3) + e, ln >> 5) * L];
+                }
+                lds4[i] = v;
+            }
         }
         __syncthreads();
         float xb = 1.0f;
@@ -1334,7 +1374,7 @@ __global__ __launch_bounds__(64 * WideGeo<F>::NW) void gru_wide_kernel(const Arg
             for (int k = 0; k < 4; ++k)
 #pragma unroll
                 for (int j = 0; j < HPW; ++j) acc[k][j] = zero;
-            wide_chain<HPW, R, Z, IN>(a.wy, ng, HT, jt0, Ys, lane, acc);
+            if (a.y) wide_chain<HPW, R, Z, IN>(a.wy, ng, HT, jt0, Ys, lane, acc);
             wide_chain<HPW, R, Z, HN>(W0, KG, HT, jt0, Hs0, lane, acc);
 #pragma unroll
             for (int j = 0; j < HPW; ++j) {
@@ -1513,17 +1553,24 @@ extern "C" int npd_gru_destroy(npd_gru* g) {
     return NPD_OK;
 }
 
-extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* is_info, int reverse, const float* gt,
-                              float* decoded, float* logits, int64_t B, void* stream) {
+extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* h0, const uint8_t* is_info, int reverse,
+                                 const float* gt, float* decoded, float* logits, int64_t B, void* stream) {
     NPD_ARG(g != nullptr, "npd_gru_decode: gru is NULL");
     NPD_ARG(B >= 0, "npd_gru_decode: B < 0");
     if (B == 0) return NPD_OK;
-    NPD_ARG(y != nullptr && decoded != nullptr && is_info != nullptr, "npd_gru_decode: null pointer");
+    NPD_ARG(decoded != nullptr && is_info != nullptr, "npd_gru_decode: null pointer");
+    NPD_ARG(y != nullptr || h0 != nullptr, "npd_gru_decode: y and h0 both NULL");
     NPD_ARG(((uintptr_t)y & 15) == 0, "npd_gru_decode: y must be 16-byte aligned");
+    NPD_ARG(h0 == nullptr || g->precision == 0 || g->img16 != nullptr,
+            "npd_gru_decode: an initial state (y_h0) needs precision 0 (fp32) or the 16-codeword split kernel "
+            "(F = 64, 2 layers, N % 32 == 0)");
+    NPD_ARG(y != nullptr || g->precision == 0 || g->img16 != nullptr,
+            "npd_gru_decode: y = NULL (y_h0) needs precision 0 (fp32) or the 16-codeword split kernel");
     gru::Args a{};
     a.img = g->img;
     a.wy = reinterpret_cast<const gru::f4*>(g->wy);
     a.y = y;
+    a.h0 = h0;
     a.gt = gt;
     a.decoded = decoded;
     a.logits = logits;
@@ -1540,7 +1587,7 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
         gru::ArgsB b{};
         b.img = g->img;
         b.wy = reinterpret_cast<const gru::f4*>(g->wy);
-        b.y = y; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
+        b.y = y; b.h0 = h0; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
         b.rev = a.rev; b.onehot = a.onehot; b.b_lin = g->b_lin; b.wy_lo = g->wy_lo;
         for (int w = 0; w < kMaxWords; ++w) b.info[w] = a.info[w];
         if (g->img16) {
@@ -1569,4 +1616,83 @@ extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* i
     if (g->F == 64) return gru::launch<64, 1>(a, s);
     if (g->layers == 2) return gru::launch<32, 2>(a, s);
     return gru::launch<32, 1>(a, s);
+}
+
+extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* is_info, int reverse, const float* gt,
+                              float* decoded, float* logits, int64_t B, void* stream) {
+    if (B > 0 && y == nullptr) return fail(NPD_EINVAL, "npd_gru_decode: null pointer");
+    return npd_gru_decode_ex(g, y, nullptr, is_info, reverse, gt, decoded, logits, B, stream);
+}
+
+// ---------------------------------------------------------------------------------- y MLP (decoding_type 'y_h0')
+// One Linear layer + activation of RNN_Model.get_h0 / get_Fy (rnn_all.py:362-385): out[b][j] = act(sum_k x[b][k]
+// W[j][k] + bias[j]), fp32, k summed in order.  64 x 64 outputs per 256-thread block (4 x 4 per thread, strided by
+// 16 so a row's 16 lanes read consecutive W rows from LDS), K in LDS-staged chunks of 16.  Once per codeword (the
+// MLP is < 2 % of a hidden-64 decode's MACs), so plain FMA, no MFMA.
+namespace npd {
+namespace gru {
+constexpr int MK = 16;
+
+__device__ __forceinline__ float mlp_act(float x, int act) {
+    switch (act) {
+        case 1: return x > 0.0f ? x : 0.0f;                                           // relu
+        case 2: return 1.0507009873554805f * (x > 0.0f ? x : 1.6732632423543772f * expm1f(x));  // selu
+        case 3: return x > 0.0f ? x : expm1f(x);                                      // elu (alpha 1)
+        case 4: return tanhf(x);
+        case 5: return 1.0f / (1.0f + expf(-x));                                      // sigmoid
+        default: return x;                                                            // linear / unknown
+    }
+}
+
+__global__ __launch_bounds__(256) void mlp_layer_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                        const float* __restrict__ bias, float* __restrict__ out,
+                                                        int64_t B, int K, int Nout, int act) {
+    __shared__ float xs[64][MK + 1];
+    __shared__ float ws[64][MK + 1];
+    const int tid = threadIdx.x;
+    const int ty = tid >> 4, tx = tid & 15;
+    const int64_t m0 = (int64_t)blockIdx.y * 64;
+    const int j0 = blockIdx.x * 64;
+    float acc[4][4] = {};
+    for (int k0 = 0; k0 < K; k0 += MK) {
+        for (int e = tid; e < 64 * MK; e += 256) {
+            const int r = e / MK, k = e % MK;
+            const int64_t m = m0 + r;
+            const int j = j0 + r;
+            xs[r][k] = (m < B && k0 + k < K) ? x[m * K + k0 + k] : 0.0f;
+            ws[r][k] = (j < Nout && k0 + k < K) ? W[(int64_t)j * K + k0 + k] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < MK; ++k)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[i][c] = fmaf(xs[ty + 16 * i][k], ws[tx + 16 * c][k], acc[i][c]);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + ty + 16 * i;
+        if (m >= B) continue;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j = j0 + tx + 16 * c;
+            if (j < Nout) out[m * Nout + j] = mlp_act(acc[i][c] + bias[j], act);
+        }
+    }
+}
+}  // namespace gru
+}  // namespace npd
+
+extern "C" int npd_ymlp_layer(const float* x, const float* W, const float* bias, float* out, int64_t B, int K, int Nout,
+                              int act, void* stream) {
+    NPD_ARG(B >= 0 && K > 0 && Nout > 0, "npd_ymlp_layer: bad sizes");
+    if (B == 0) return NPD_OK;
+    NPD_ARG(x != nullptr && W != nullptr && bias != nullptr && out != nullptr, "npd_ymlp_layer: null pointer");
+    NPD_ARG(act >= 0 && act <= 5, "npd_ymlp_layer: act must be 0 (linear), 1 relu, 2 selu, 3 elu, 4 tanh, 5 sigmoid");
+    NPD_ARG(B <= (int64_t)65535 * 64, "npd_ymlp_layer: B too large for one launch (split the batch)");
+    dim3 grid((unsigned)((Nout + 63) / 64), (unsigned)((B + 63) / 64));
+    hipLaunchKernelGGL(gru::mlp_layer_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, W, bias, out, B, K, Nout, act);
+    return launch_check("mlp_layer_kernel launch");
 }

@@ -18,9 +18,9 @@ from . import _lib
 
 
 class RNN_Model(nn.Module):
-    """Same parameters as the reference (rnn_all.py:294-385).  Only the configuration the CRISP
-    y_input eval uses is accepted by the fused decoder: GRU, output_size 1, y_depth 0,
-    out_linear_depth 1, unidirectional, no layernorm."""
+    """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts GRU nets with output_size 1,
+    out_linear_depth 1, unidirectional, no layernorm: decoding_type 'y_input' with y_depth 0 (the CRISP scripts,
+    rnn_all.py:250-253) and 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip)."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -41,6 +41,12 @@ class RNN_Model(nn.Module):
         self.skip = skip
         self.rnn = getattr(nn, rnn_type)(input_size, feature_size, num_rnn_layers, bidirectional=bidirectional,
                                          batch_first=True)
+        self.y_output_size = ((int(bidirectional) + 1) * num_rnn_layers * feature_size if y_output_size is None
+                              else y_output_size)
+        if y_hidden_size > 0 and y_depth > 0:  # rnn_all.py:323-329, same module order and names
+            self.y_linears = nn.ModuleList([nn.Linear(y_size, y_hidden_size, bias=True)])
+            self.y_linears.extend([nn.Linear(y_hidden_size, y_hidden_size, bias=True) for _ in range(1, y_depth - 1)])
+            self.y_linears.append(nn.Linear(y_hidden_size, self.y_output_size - (y_size if skip else 0), bias=True))
         self.drop = nn.Dropout(dropout)
         self.layernorm = nn.LayerNorm(feature_size) if use_layernorm else nn.Identity()
         if out_linear_depth == 1:
@@ -52,6 +58,27 @@ class RNN_Model(nn.Module):
             layers += [nn.SELU(), nn.Linear(y_hidden_size, output_size)]
             self.linear = nn.Sequential(*layers)
 
+    ACTS = {"linear": 0, "relu": 1, "selu": 2, "elu": 3, "tanh": 4, "sigmoid": 5}
+
+    def act(self, inputs):
+        """rnn_all.py:346-360 (an unknown name is the identity)."""
+        import torch.nn.functional as Fn
+        fn = {"tanh": torch.tanh, "elu": Fn.elu, "relu": Fn.relu, "selu": Fn.selu, "sigmoid": torch.sigmoid}
+        return fn.get(self.activation, lambda x: x)(inputs)
+
+    def get_h0(self, y):
+        """rnn_all.py:362-375 in PyTorch, reference semantics: layer ii is followed by act iff ii != y_depth (every
+        layer, the last included, for y_depth >= 2; all but the last for y_depth = 1).  The fused decoder runs this
+        MLP on npd_ymlp_layer instead."""
+        x = y.clone()
+        for ii, layer in enumerate(self.y_linears):
+            x = layer(x) if ii == self.y_depth else self.act(layer(x))
+        if self.skip:
+            x = torch.cat([y, x], 1)
+        x = x.reshape(-1, self.feature_size, (int(self.bidirectional) + 1) * self.num_rnn_layers).permute(2, 0, 1)
+        x = x.contiguous()
+        return x if self.rnn_type == "GRU" else (x, x)
+
     def forward(self, input, hidden, Fy=None):
         """Single recurrent step (rnn_all.py:387-398) -- the training-time API."""
         out, hidden = self.rnn(input, hidden)
@@ -59,19 +86,27 @@ class RNN_Model(nn.Module):
         decoded = self.linear(out if Fy is None else torch.cat([Fy, out], -1))
         return decoded.view(-1, self.output_size), hidden
 
-    def fused_supported(self) -> bool:
-        return (self.rnn_type == "GRU" and self.output_size == 1 and self.y_depth == 0 and self.out_linear_depth == 1
+    def fused_supported(self, decoding_type="y_input") -> bool:
+        base = (self.rnn_type == "GRU" and self.output_size == 1 and self.out_linear_depth == 1
                 and not self.bidirectional and isinstance(self.layernorm, nn.Identity)
                 and self.feature_size in (32, 64, 128, 256, 512) and self.num_rnn_layers in (1, 2))
+        if decoding_type == "y_h0":
+            return (base and hasattr(self, "y_linears") and not self.skip and self.activation in self.ACTS
+                    and self.y_output_size == self.num_rnn_layers * self.feature_size)
+        return base and self.y_depth == 0
 
 
-def pack_gru_weights(net: nn.Module, layers: int) -> np.ndarray:
-    """Flatten the state dict in the order of include/npd.h npd_gru_create."""
+def pack_gru_weights(net: nn.Module, layers: int, y_cols: int = 0) -> np.ndarray:
+    """Flatten the state dict in the order of include/npd.h npd_gru_create; y_cols > 0 ('y_h0'): weight_ih_l0 gets
+    y_cols zero columns in front (the y_input layout with no y)."""
     sd = net.state_dict()
     parts = []
     for l in range(layers):
         for nm in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
-            parts.append(sd[f"rnn.{nm}_l{l}"].detach().float().cpu().numpy().ravel())
+            w = sd[f"rnn.{nm}_l{l}"].detach().float().cpu().numpy()
+            if nm == "weight_ih" and l == 0 and y_cols:
+                w = np.concatenate([np.zeros((w.shape[0], y_cols), np.float32), w], 1)
+            parts.append(w.ravel())
     parts.append(sd["linear.weight"].detach().float().cpu().numpy().ravel())
     parts.append(sd["linear.bias"].detach().float().cpu().numpy().ravel())
     return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
@@ -119,12 +154,12 @@ class RNN_decoder:
 
     def _handle(self, net: RNN_Model, device):
         # re-pack when the weights change (parameter versions) or the device differs
-        key = (id(net), str(device), self.precision, tuple(p._version for p in net.parameters()),
+        key = (id(net), str(device), self.precision, self.decoding_type, tuple(p._version for p in net.parameters()),
                tuple(p.data_ptr() for p in net.parameters()))
         h = self._cache.get(key)
         if h is None:
             self._cache.clear()
-            W = pack_gru_weights(net, net.num_rnn_layers)
+            W = pack_gru_weights(net, net.num_rnn_layers, self.N if self.decoding_type == "y_h0" else 0)
             with torch.cuda.device(device):
                 h = _GruHandle(self.N, net.feature_size, net.num_rnn_layers, self.onehot, W,
                                self.PRECISIONS[self.precision])
@@ -135,12 +170,14 @@ class RNN_decoder:
         if train:
             raise _lib.NpdError("RNN_decoder.decode(train=True) is the training path (out of scope for the fused "
                                 "decoder); use the reference's PyTorch loop for training")
-        if self.decoding_type != "y_input":
-            raise _lib.NpdError(f"fused decode supports decoding_type 'y_input', got {self.decoding_type!r}")
-        if not (hasattr(net, "fused_supported") and net.fused_supported()):
+        if self.decoding_type not in ("y_input", "y_h0"):
+            raise _lib.NpdError(f"fused decode supports decoding_type 'y_input' and 'y_h0', got {self.decoding_type!r}"
+                                " ('y_h0_out' builds a (1 + depth) F y-MLP that get_h0 cannot reshape, rnn_all.py:1324)")
+        if not (hasattr(net, "fused_supported") and net.fused_supported(self.decoding_type)):
             raise _lib.NpdError("network configuration not supported by the fused GRU decoder")
-        if net.input_size != self.N + 1 + int(self.onehot):
-            raise ValueError("net.input_size must be N + 1 + onehot")
+        din = (self.N if self.decoding_type == "y_input" else 0) + 1 + int(self.onehot)
+        if net.input_size != din:
+            raise ValueError(f"net.input_size must be {'N + ' if self.decoding_type == 'y_input' else ''}1 + onehot")
         y_in = y
         y = _lib.f32c(_lib.stage(y, "y"))
         B = y.shape[0]
@@ -152,11 +189,37 @@ class RNN_decoder:
         dec = torch.empty(B, self.N, dtype=torch.float32, device=y.device)
         logits = torch.empty(B, self.N, dtype=torch.float32, device=y.device) if return_logits else None
         g = None if gt is None else _lib.f32c(_lib.stage(gt, "gt", y.device))
-        _lib.check(_lib.load().npd_gru_decode(h.h, _lib.ptr(y), is_info.ctypes.data_as(ctypes.c_void_p),
-                                              1 if self.reverse_order else 0, _lib.ptr(g), _lib.ptr(dec),
-                                              _lib.ptr(logits), B, _lib.stream_of(y.device)), "npd_gru_decode")
+        h0 = self._h0(net, y) if self.decoding_type == "y_h0" else None
+        _lib.check(_lib.load().npd_gru_decode_ex(h.h, None if h0 is not None else _lib.ptr(y), _lib.ptr(h0),
+                                                 is_info.ctypes.data_as(ctypes.c_void_p),
+                                                 1 if self.reverse_order else 0, _lib.ptr(g), _lib.ptr(dec),
+                                                 _lib.ptr(logits), B, _lib.stream_of(y.device)), "npd_gru_decode")
         dec = _lib.home(dec, y_in)
         return (dec, _lib.home(logits, y_in)) if return_logits else dec
+
+    def _h0(self, net, y):
+        """(B, F * layers) initial states: get_h0's MLP, kept alive past the stream-ordered decode by the caller."""
+        return _ymlp_forward(net, y)
+
+
+def _ymlp_forward(net: RNN_Model, y: torch.Tensor) -> torch.Tensor:
+    """get_h0's MLP (rnn_all.py:362-375) on npd_ymlp_layer: (B, N) -> (B, F * layers), layer ii followed by the
+    activation iff ii != y_depth (RNN_Model.get_h0).  Returns x before the reshape: element f * layers + l = layer l's
+    initial state of unit f."""
+    L = _lib.load()
+    x = y
+    step = 65535 * 64
+    for ii, layer in enumerate(net.y_linears):
+        act = 0 if ii == net.y_depth else RNN_Model.ACTS[net.activation]
+        W = _lib.f32c(layer.weight.detach().to(y.device))
+        b = _lib.f32c(layer.bias.detach().to(y.device))
+        out = torch.empty(y.shape[0], W.shape[0], dtype=torch.float32, device=y.device)
+        for s0 in range(0, y.shape[0], step):
+            xs, os_ = x[s0:s0 + step], out[s0:s0 + step]
+            _lib.check(L.npd_ymlp_layer(_lib.ptr(xs), _lib.ptr(W), _lib.ptr(b), _lib.ptr(os_), xs.shape[0],
+                                        W.shape[1], W.shape[0], act, _lib.stream_of(y.device)), "npd_ymlp_layer")
+        x = out
+    return x
 
 
 def get_onehot(actions):

@@ -440,6 +440,44 @@ def gen_gru(cases=None):
              logits=np.concatenate(logits), info=info, N=N, K=K, F=F, onehot=int(onehot), rev=int(rev), **extra)
 
 
+def gen_gru_yh0():
+    """decoding_type 'y_h0' (rnn_all.py:73 default; decode test branch rnn_all.py:523-531): hidden = get_h0(y) through
+    the y-MLP (y_linears, layer ii followed by RNN_Model.act iff ii != y_depth), then the RNN input is onehot(previous decision) alone.
+    PyTorch-default seeded weights (torch.manual_seed(seed)), Polar codes, words from the reference's encoder and
+    channel at 0-4 dB; logits recorded with a forward hook on net.linear."""
+    cases = [("gru_yh0_polar_64_32", 64, 32, 64, 2, True, False, "selu", 128, 3, 512, 3001),
+             ("gru_yh0_polar_32_16_f128_relu_rev", 32, 16, 128, 2, True, True, "relu", 64, 2, 256, 3002),
+             ("gru_yh0_polar_16_8_l1_tanh_noonehot", 16, 8, 32, 1, False, False, "tanh", 32, 4, 256, 3003),
+             ("gru_yh0_polar_32_16_elu_d1", 32, 16, 64, 2, True, False, "elu", 48, 1, 256, 3004),
+             ("gru_yh0_polar_16_8_sigmoid", 16, 8, 32, 2, True, False, "sigmoid", 16, 3, 128, 3005)]
+    for name, N, K, F, L, onehot, rev, act, yh, yd, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        net = rnn_m.RNN_Model("GRU", 1 + int(onehot), F, 1, L, N, yh, yd, act, 0.0, False)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_h0", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits, h0s = [], [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+                h0 = net.get_h0(y)  # (L, B, F)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+            h0s.append(h0.permute(1, 2, 0).reshape(y.shape[0], -1).numpy())  # x layout: f * L + l
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), h0x=np.concatenate(h0s), info=info, N=N, K=K, F=F, layers=L,
+             onehot=int(onehot), rev=int(rev), activation=np.bytes_(act), y_hidden=yh, y_depth=yd,
+             **{"w." + k: v for k, v in sd.items()})
+
+
 # ------------------------------------------------------------------------------------------- conv
 def conv_weights_from_seed(embed, N, seed):
     """Documented deterministic generator (mirrored in tests/conftest.py): PCG64(seed); each parameter,
@@ -485,6 +523,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "conv"]
     for w in which:
         globals()["gen_" + w]()
