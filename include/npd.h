@@ -228,6 +228,15 @@ int npd_gru_create(int N, int F, int layers, int onehot, const float* weights, i
                    npd_gru** out);
 int npd_gru_destroy(npd_gru* gru);
 /*
+ * npd_gru_create for either cell of rnn_all.py:69 (--rnn_type GRU | LSTM): cell 0 = GRU (npd_gru_create), cell 1 =
+ * LSTM (nn.LSTM, gates i, f, g, o; the same weight order with 4F gate rows: weight_ih_l (4F, Din_l) | weight_hh_l (4F, F)
+ * | bias_ih_l (4F) | bias_hh_l (4F) per layer, then linear.weight | linear.bias).  LSTM: fp32 (precision 0), hidden 32
+ * (1 or 2 layers) or 64 (1 layer: at 2 layers its weights exceed the 160 KB LDS), y_input decoding (npd_gru_decode;
+ * destroy with npd_gru_destroy).
+ */
+int npd_rnn_create(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
+                   npd_gru** out);
+/*
  * RNN_decoder.decode(net, False, y, gt) test branch (rnn_all.py:532-547): decoded (B,N) fp32, with
  * decoded[:, i] = sign(out_i) for i in the info set (is_info: N bytes, host) and 1 (or gt) else.
  * reverse: RNN_decoder reverse_order (rnn_all.py:414-416).  logits (B,N) optional: raw output at

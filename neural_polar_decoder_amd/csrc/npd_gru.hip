@@ -34,6 +34,7 @@ struct npd_gru {
     float* wy16;
     int64_t wy16_lo;
     int split16;   // its SplitT variant
+    int cell;      // 0 GRU, 1 LSTM (fp32, F <= 64)
 };
 
 namespace npd {
@@ -441,6 +442,211 @@ static int launch(const Args& a, hipStream_t s) {
     const int grid = grid_for(wgs, 1, device_cu_count());
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WPB), lds, s, a);
     return launch_check("gru_decode_kernel launch");
+}
+
+// =============================================================================== LSTM cells (fp32, F <= 64)
+// rnn_all.py:69 offers --rnn_type LSTM; RNN_decoder's y_input test branch then carries (h, c) pairs (rnn_all.py:536-547)
+// through nn.LSTM: gates i, f, g, o (PyTorch row order) = W_ih x + b_ih + W_hh h + b_hh, c' = sig(f) c + sig(i) tanh(g),
+// h' = sig(o) tanh(c').  Same layout as gru_decode_kernel with 4F gate rows: images [L0 hh | L1 ih | L1 hh] of 4F x F in
+// A-operand order, every gate row pre-multiplied by its exp2 constant (i, f, o: -log2 e; g: -2 log2 e), all biases
+// (+ the one-hot column 0 on layer 0) as accumulator initialisation, the x_i column one [1, x_i] k-step on layer 0.
+template <int F, int L>
+struct LGeo {
+    static constexpr int TT = 4 * F / 32;
+    static constexpr int HT = F / 32;
+    static constexpr int KS = F / 2;
+    static constexpr int KG = KS / 4;
+    static constexpr int NG = (L == 2) ? 3 : 1;
+    static constexpr int G_SIZE = TT * KG * 64 * 4;
+    static constexpr int OFF_X = NG * G_SIZE;           // layer-0 [1, x_i] k-step A operands [TT][64]
+    static constexpr int OFF_WL = OFF_X + TT * 64;       // linear weights [half][HT][16]
+    static constexpr int OFF_CV = OFF_WL + 2 * HT * 16;  // bias tiles in accumulator order: [layer][TT][half][16]
+    static constexpr int TOTAL = OFF_CV + L * TT * 32;
+};
+
+__device__ __forceinline__ float sig2(float a) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a)); }
+
+template <int F, int L>
+__global__ __launch_bounds__(64 * NPD_GRU_WPB) void lstm_decode_kernel(const Args a) {
+    using G = LGeo<F, L>;
+    constexpr int TT = G::TT, HT = G::HT, KG = G::KG;
+    extern __shared__ __attribute__((aligned(16))) f4 smem4[];
+    const float* smem = reinterpret_cast<const float*>(smem4);
+    {
+        const f4* src = reinterpret_cast<const f4*>(a.img);
+        for (int i = threadIdx.x; i < G::TOTAL / 4; i += blockDim.x) smem4[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int half = lane >> 5;
+    const int col = lane & 31;
+    const int N = a.N;
+    const int64_t ntiles = (a.B + 31) / 32;
+    const f16v zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto cvec = [&](int off) -> f16v {
+        const f4* p = reinterpret_cast<const f4*>(smem + off + half * 16);
+        const f4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        return f16v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                    x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+    };
+    constexpr float kT = -2.88539008177792681472f;  // tanh(c) = 2 sig2(kT c) - 1
+    for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU_WPB + wave; tile < ntiles; tile += (int64_t)gridDim.x * NPD_GRU_WPB) {
+        const int64_t cw = tile * 32 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        f16v P[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) P[t] = cvec(G::OFF_CV + t * 32);
+        {
+            const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
+            const int ng = N / 8;
+            for (int s4 = 0; s4 < ng; ++s4) {
+                const f4 yv = yr[s4];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const f4 w = a.wy[(t * ng + s4) * 64 + lane];
+                    P[t] = mfma(w.x, yv.x, P[t]);
+                    P[t] = mfma(w.y, yv.y, P[t]);
+                    P[t] = mfma(w.z, yv.z, P[t]);
+                    P[t] = mfma(w.w, yv.w, P[t]);
+                }
+            }
+        }
+        f16v h0[HT], c0[HT], h1[HT], c1[HT];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+            h0[t] = zero;
+            c0[t] = zero;
+            h1[t] = zero;
+            c1[t] = zero;
+        }
+        float xb = 1.0f;
+        auto cell = [&](f16v& h, f16v& c, const f16v (&acc)[TT], int j) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float ig = sig2(acc[j][i]), fg = sig2(acc[HT + j][i]);
+                const float gg = fmaf(2.0f, sig2(acc[2 * HT + j][i]), -1.0f);
+                const float og = sig2(acc[3 * HT + j][i]);
+                c[i] = fmaf(fg, c[i], ig * gg);
+                h[i] = og * fmaf(2.0f, sig2(kT * c[i]), -1.0f);
+            }
+        };
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            const float xbe = half ? xb : 1.0f;
+            {
+                f16v acc[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = mfma(smem[G::OFF_X + t * 64 + lane], xbe, P[t]);
+                gemm_chain<TT, KG, TT, HT>(smem4, 0, 0, lane, acc, h0);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) cell(h0[j], c0[j], acc, j);
+            }
+            if constexpr (L == 2) {
+                f16v acc1[TT];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc1[t] = cvec(G::OFF_CV + (TT + t) * 32);
+                gemm_chain<TT, KG, TT, HT>(smem4, 1, 0, lane, acc1, h0);
+                gemm_chain<TT, KG, TT, HT>(smem4, 2, 0, lane, acc1, h1);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) cell(h1[j], c1[j], acc1, j);
+            }
+            float part = 0.0f;
+#pragma unroll
+            for (int t = 0; t < HT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) part += smem[G::OFF_WL + (half * HT + t) * 16 + i] * (L == 2 ? h1[t][i] : h0[t][i]);
+            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+            float d;
+            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+            if (half == 0 && valid) {
+                a.decoded[cw * N + jj] = d;
+                if (a.logits) a.logits[cw * N + ii] = out;
+            }
+            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+        }
+    }
+}
+
+// host image of lstm_decode_kernel from the npd_gru_create weight order with 4F gate rows
+template <int F, int L>
+static void build_image_lstm(const float* W, int N, int onehot, std::vector<float>& img, std::vector<float>& wy,
+                             float& b_lin) {
+    using G = LGeo<F, L>;
+    constexpr int TT = G::TT, HT = G::HT, KG = G::KG, KS = G::KS;
+    const int Din = N + (onehot ? 2 : 1);
+    const float* p = W;
+    const float *wih[2], *whh[2], *bih[2], *bhh[2];
+    for (int l = 0; l < L; ++l) {
+        const int din = l == 0 ? Din : F;
+        wih[l] = p; p += (size_t)4 * F * din;
+        whh[l] = p; p += (size_t)4 * F * F;
+        bih[l] = p; p += 4 * F;
+        bhh[l] = p; p += 4 * F;
+    }
+    const float* wlin = p;
+    b_lin = p[F];
+    img.assign(G::TOTAL, 0.0f);
+    auto fr = [&](int row) { return (row >= 2 * F && row < 3 * F) ? -2.88539008177792681472f : -1.44269504088896340736f; };
+    const float* mats[3] = {whh[0], L == 2 ? wih[1] : nullptr, L == 2 ? whh[1] : nullptr};
+    for (int g = 0; g < G::NG; ++g)
+        for (int t = 0; t < TT; ++t)
+            for (int s = 0; s < KS; ++s)
+                for (int l = 0; l < 64; ++l) {
+                    const int row = 32 * t + (l & 31);
+                    img[((size_t)(g * TT + t) * KG + s / 4) * 256 + l * 4 + (s & 3)] =
+                        fr(row) * mats[g][(size_t)row * F + hid_of(s, l >> 5)];
+                }
+    // layer-0 [1, x_i] k-step: half 0 pairs with 1 (nothing left: the one-hot column 0 is in the bias tile), half 1
+    // with x_i (one-hot: column 1 - column 0; sign input: its column)
+    for (int t = 0; t < TT; ++t)
+        for (int l = 32; l < 64; ++l) {
+            const int row = 32 * t + (l & 31);
+            const float v = onehot ? wih[0][(size_t)row * Din + N + 1] - wih[0][(size_t)row * Din + N]
+                                   : wih[0][(size_t)row * Din + N];
+            img[G::OFF_X + t * 64 + l] = fr(row) * v;
+        }
+    for (int hf = 0; hf < 2; ++hf)
+        for (int t = 0; t < HT; ++t)
+            for (int i = 0; i < 16; ++i) img[G::OFF_WL + (hf * HT + t) * 16 + i] = wlin[32 * t + (i & 3) + 8 * (i >> 2) + 4 * hf];
+    for (int l = 0; l < L; ++l)
+        for (int t = 0; t < TT; ++t)
+            for (int hf = 0; hf < 2; ++hf)
+                for (int i = 0; i < 16; ++i) {
+                    const int row = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hf;
+                    float v = bih[l][row] + bhh[l][row];
+                    if (l == 0 && onehot) v += wih[0][(size_t)row * Din + N];
+                    img[G::OFF_CV + ((l * TT + t) * 2 + hf) * 16 + i] = fr(row) * v;
+                }
+    const int ng = N / 8;
+    wy.assign((size_t)TT * ng * 256, 0.0f);
+    for (int t = 0; t < TT; ++t)
+        for (int s = 0; s < N / 2; ++s)
+            for (int l = 0; l < 64; ++l) {
+                const int row = 32 * t + (l & 31);
+                const int k = s + (l >> 5) * (N / 2);
+                wy[((size_t)t * ng + s / 4) * 256 + l * 4 + (s & 3)] = fr(row) * wih[0][(size_t)row * Din + k];
+            }
+}
+
+template <int F, int L>
+static int launch_lstm(const Args& a, hipStream_t s) {
+    using G = LGeo<F, L>;
+    auto kern = lstm_decode_kernel<F, L>;
+    const size_t lds = (size_t)G::TOTAL * 4;
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    const int64_t tiles = (a.B + 31) / 32;
+    const int64_t wgs = (tiles + NPD_GRU_WPB - 1) / NPD_GRU_WPB;
+    hipLaunchKernelGGL(kern, dim3(grid_for(wgs, 1, device_cu_count())), dim3(64 * NPD_GRU_WPB), lds, s, a);
+    return launch_check("lstm_decode_kernel launch");
 }
 
 // =============================================================================== split 16-bit MFMA paths
@@ -1464,6 +1670,54 @@ static int launch_wide(const Args& a, int N, hipStream_t s) {
 
 using namespace npd;
 
+static int create_lstm(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
+                       npd_gru** out) {
+    NPD_ARG(F == 32 || F == 64, "npd_rnn_create: LSTM cells cover hidden sizes 32 and 64");
+    NPD_ARG(F == 32 || layers == 1,
+            "npd_rnn_create: an LSTM with hidden 64 and 2 layers needs 192 KB of LDS-resident weights (160 KB per CU)");
+    NPD_ARG(precision == 0, "npd_rnn_create: LSTM cells run fp32 (precision 0)");
+    const int Din = N + (onehot ? 2 : 1);
+    int64_t expect = (int64_t)4 * F * Din + (int64_t)4 * F * F + 8 * F;
+    if (layers == 2) expect += (int64_t)8 * F * F + 8 * F;
+    expect += F + 1;
+    NPD_ARG(n_weights == expect, "npd_rnn_create: weight count does not match (LSTM, N, F, layers, onehot)");
+    std::vector<float> img, wy;
+    float b_lin = 0.0f;
+    if (F == 64) gru::build_image_lstm<64, 1>(weights, N, onehot, img, wy, b_lin);
+    else if (layers == 2) gru::build_image_lstm<32, 2>(weights, N, onehot, img, wy, b_lin);
+    else gru::build_image_lstm<32, 1>(weights, N, onehot, img, wy, b_lin);
+    npd_gru* g = new (std::nothrow) npd_gru;
+    if (!g) return fail(NPD_ENOMEM, "npd_rnn_create: out of memory");
+    memset(g, 0, sizeof(*g));
+    g->N = N; g->F = F; g->layers = layers; g->onehot = onehot; g->precision = 0; g->b_lin = b_lin; g->cell = 1;
+    g->img_floats = (int64_t)img.size();
+    hipError_t e = hipGetDevice(&g->device);
+    if (e == hipSuccess) e = hipMalloc(&g->img, img.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&g->wy, wy.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(g->img, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(g->wy, wy.data(), wy.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (g->img) (void)hipFree(g->img);
+        if (g->wy) (void)hipFree(g->wy);
+        delete g;
+        return hip_fail(e, "npd_rnn_create");
+    }
+    *out = g;
+    return NPD_OK;
+}
+
+extern "C" int npd_rnn_create(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights,
+                              int precision, npd_gru** out) {
+    NPD_ARG(out != nullptr, "npd_rnn_create: out is NULL");
+    *out = nullptr;
+    NPD_ARG(cell == 0 || cell == 1, "npd_rnn_create: cell must be 0 (GRU) or 1 (LSTM)");
+    if (cell == 0) return npd_gru_create(N, F, layers, onehot, weights, n_weights, precision, out);
+    NPD_ARG(weights != nullptr, "npd_rnn_create: weights is NULL");
+    NPD_ARG(N >= 8 && N <= kMaxN && N % 8 == 0, "npd_rnn_create: N must be a multiple of 8 in [8, 256]");
+    NPD_ARG(layers == 1 || layers == 2, "npd_rnn_create: 1 or 2 layers supported");
+    return create_lstm(N, F, layers, onehot, weights, n_weights, precision, out);
+}
+
 extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights,
                               int precision, npd_gru** out) {
     NPD_ARG(out != nullptr, "npd_gru_create: out is NULL");
@@ -1566,6 +1820,8 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
             "(F = 64, 2 layers, N % 32 == 0)");
     NPD_ARG(y != nullptr || g->precision == 0 || g->img16 != nullptr,
             "npd_gru_decode: y = NULL (y_h0) needs precision 0 (fp32) or the 16-codeword split kernel");
+    NPD_ARG(g->cell == 0 || (y != nullptr && h0 == nullptr),
+            "npd_gru_decode: LSTM cells decode y_input (y given, no initial state)");
     gru::Args a{};
     a.img = g->img;
     a.wy = reinterpret_cast<const gru::f4*>(g->wy);
@@ -1583,6 +1839,10 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
     for (int i = 0; i < g->N; ++i)
         if (is_info[i]) a.info[i >> 5] |= 1u << (i & 31);
     hipStream_t s = (hipStream_t)stream;
+    if (g->cell == 1) {
+        if (g->F == 64) return gru::launch_lstm<64, 1>(a, s);
+        return g->layers == 2 ? gru::launch_lstm<32, 2>(a, s) : gru::launch_lstm<32, 1>(a, s);
+    }
     if (g->precision != 0) {
         gru::ArgsB b{};
         b.img = g->img;

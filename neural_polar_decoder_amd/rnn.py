@@ -18,9 +18,10 @@ from . import _lib
 
 
 class RNN_Model(nn.Module):
-    """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts GRU nets with output_size 1,
-    out_linear_depth 1, unidirectional, no layernorm: decoding_type 'y_input' with y_depth 0 (the CRISP scripts,
-    rnn_all.py:250-253) and 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip)."""
+    """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts nets with output_size 1,
+    out_linear_depth 1, unidirectional, no layernorm: GRU with decoding_type 'y_input' and y_depth 0 (the CRISP
+    scripts, rnn_all.py:250-253) or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip);
+    LSTM (rnn_all.py:69) with 'y_input', fp32, hidden 32 or hidden 64 with one layer."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -87,9 +88,12 @@ class RNN_Model(nn.Module):
         return decoded.view(-1, self.output_size), hidden
 
     def fused_supported(self, decoding_type="y_input") -> bool:
-        base = (self.rnn_type == "GRU" and self.output_size == 1 and self.out_linear_depth == 1
-                and not self.bidirectional and isinstance(self.layernorm, nn.Identity)
-                and self.feature_size in (32, 64, 128, 256, 512) and self.num_rnn_layers in (1, 2))
+        common = (self.output_size == 1 and self.out_linear_depth == 1 and not self.bidirectional
+                  and isinstance(self.layernorm, nn.Identity) and self.num_rnn_layers in (1, 2))
+        if self.rnn_type == "LSTM":  # fp32 lstm_decode_kernel: hidden 32, or 64 with one layer (LDS-resident weights)
+            return (common and decoding_type == "y_input" and self.y_depth == 0
+                    and (self.feature_size == 32 or (self.feature_size == 64 and self.num_rnn_layers == 1)))
+        base = common and self.rnn_type == "GRU" and self.feature_size in (32, 64, 128, 256, 512)
         if decoding_type == "y_h0":
             return (base and hasattr(self, "y_linears") and not self.skip and self.activation in self.ACTS
                     and self.y_output_size == self.num_rnn_layers * self.feature_size)
@@ -113,11 +117,12 @@ def pack_gru_weights(net: nn.Module, layers: int, y_cols: int = 0) -> np.ndarray
 
 
 class _GruHandle:
-    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0):
+    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0, cell=0):
         L = _lib.load()
         out = ctypes.c_void_p()
-        _lib.check(L.npd_gru_create(int(N), int(F), int(layers), 1 if onehot else 0, W.ctypes.data_as(ctypes.c_void_p),
-                                    int(W.size), int(precision), ctypes.byref(out)), "npd_gru_create")
+        _lib.check(L.npd_rnn_create(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
+                                    W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision), ctypes.byref(out)),
+                   "npd_rnn_create")
         self.h = out
 
     def __del__(self):
@@ -162,7 +167,7 @@ class RNN_decoder:
             W = pack_gru_weights(net, net.num_rnn_layers, self.N if self.decoding_type == "y_h0" else 0)
             with torch.cuda.device(device):
                 h = _GruHandle(self.N, net.feature_size, net.num_rnn_layers, self.onehot, W,
-                               self.PRECISIONS[self.precision])
+                               self.PRECISIONS[self.precision], 1 if net.rnn_type == "LSTM" else 0)
             self._cache[key] = h
         return h
 

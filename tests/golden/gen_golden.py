@@ -478,6 +478,37 @@ def gen_gru_yh0():
              **{"w." + k: v for k, v in sd.items()})
 
 
+def gen_lstm():
+    """--rnn_type LSTM (rnn_all.py:69) with decoding_type y_input (rnn_all.py:532-547: hidden = (h, c) zeros): seeded
+    PyTorch-default weights, Polar codes, reference encoder / channel at 0-4 dB, logits by a hook on net.linear."""
+    cases = [("lstm_polar_64_32_f64_l1", 64, 32, 64, 1, True, False, 512, 4001),
+             ("lstm_polar_32_16_f32_l2_rev", 32, 16, 32, 2, True, True, 256, 4002),
+             ("lstm_polar_16_8_f32_l1_noonehot", 16, 8, 32, 1, False, False, 256, 4003)]
+    for name, N, K, F, L, onehot, rev, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        net = rnn_m.RNN_Model("LSTM", N + 1 + int(onehot), F, 1, L, N, 0, 0, "selu", 0.0, False)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_input", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits = [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, layers=L, onehot=int(onehot), rev=int(rev),
+             **{"w." + k: v for k, v in sd.items()})
+
+
 # ------------------------------------------------------------------------------------------- conv
 def conv_weights_from_seed(embed, N, seed):
     """Documented deterministic generator (mirrored in tests/conftest.py): PCG64(seed); each parameter,
@@ -523,6 +554,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "lstm", "conv"]
     for w in which:
         globals()["gen_" + w]()
