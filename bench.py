@@ -318,8 +318,9 @@ PMC_GRU_JSON = os.path.join(ROOT, "profiles", "round4", "pmc_gru_summary.json")
 def split_issue_bound(ms16, B, steps):
     """Combined MFMA + VALU issue bound of gru16p_kernel from its committed PMC (profiles/round4/pmc_gru_summary.json):
     the two serialise on a SIMD (profiles/round3/coissue.txt), so the kernel needs at least (MFMA busy + VALU busy)
-    cycles per SIMD.  Per wave-step cycles from the counters, scaled to this launch, over the clock the chip holds
-    (GRBM_GUI_ACTIVE / 8 / kernel time of the PMC run) and over the 2.4 GHz the spec peaks assume."""
+    cycles per SIMD.  Per wave-step cycles from the counters, scaled to this launch, over the clock the chip held in
+    the PMC run (GRBM_GUI_ACTIVE / 8 / kernel time) and over the 2.4 GHz the spec peaks assume; frac = ceiling time /
+    this launch's time (above 1 at the PMC run's clock when this run holds a higher one)."""
     if not os.path.exists(PMC_GRU_JSON):
         return None
     pm = json.load(open(PMC_GRU_JSON))
@@ -328,11 +329,15 @@ def split_issue_bound(ms16, B, steps):
         return None
     ws = k["per_wave_step"]  # mfma_cycles, valu_cycles per 16-codeword wave and decoding step
     simds = 1024
-    cycles = (ws["mfma_cycles"] + ws["valu_cycles"]) * (B / 16) * steps / simds
+    # each v_mfma_f32_16x16x32_f16 (16 busy cycles) also holds vector issue for 4 of the cycles SQ_ACTIVE_INST_VALU
+    # counts, so those are in both counters once: serialised cycles = MFMA busy + VALU active - 4 x MFMA count
+    serial = ws["mfma_cycles"] + ws["valu_cycles"] - 4.0 * ws["mfma_cycles"] / 16.0
+    cycles = serial * (B / 16) * steps / simds
     at_held = cycles / (k["clock_ghz"] * 1e9) * 1e3
     at_spec = cycles / 2.4e9 * 1e3
     return {"bound": "mfma + valu issue (serialised on the SIMD)", "pmc": "profiles/round4/pmc_gru_summary.json",
             "mfma_cycles_per_wave_step": ws["mfma_cycles"], "valu_cycles_per_wave_step": ws["valu_cycles"],
+            "serialised_cycles_per_wave_step": serial,
             "ceiling_ms_at_2.4GHz": at_spec, "ceiling_ms_at_held_clock": at_held, "held_clock_ghz": k["clock_ghz"],
             "frac_at_2.4GHz": at_spec / ms16, "frac_at_held_clock": at_held / ms16}
 
