@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void conv_layer_split_kernel(const float* __re
 // hi / lo LDS slab after them, so HBM reads overlap the matrix work and no weight fragment is re-read.  Dilation <= 4
 // (conv_spec) bounds the halo at 12.
 template <int NG, int Q, int KS, int NW>
-__global__ __launch_bounds__(64 * NW) void conv_split_ws_kernel(const float* __restrict__ in, float* __restrict__ out,
+__global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_split_ws_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                                 const float* __restrict__ res,
                                                                 const f4* __restrict__ wimg,
                                                                 const float* __restrict__ bias, int cin, int cout,
@@ -282,6 +282,8 @@ __global__ __launch_bounds__(64 * NW) void conv_split_ws_kernel(const float* __r
     constexpr int PS = NW / 2 / KS;   // position parts
     constexpr int TPW = 2 * Q / PS;   // 32-position tiles per wave
     static_assert(NG % KS == 0 && (NW / 2) % KS == 0 && (2 * Q) % PS == 0, "wave decomposition");
+    // partial-sum slots per wave: KS = 2 with 2 tiles hands over exactly one (slot 0), else slot = tile
+    constexpr int RS = (KS == 2 && TPW == 2) ? 1 : TPW;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(64 * NW) void conv_split_ws_kernel(const float* __r
             for (int q = 0; q < TPW; ++q)
                 if (q % KS != kp)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) red[((wave * TPW + q) * 16 + r) * 64 + lane] = acc[q][r];
+                    for (int r = 0; r < 16; ++r) red[((wave * RS + (RS == 1 ? 0 : q)) * 16 + r) * 64 + lane] = acc[q][r];
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < TPW; ++q)
@@ -389,7 +391,8 @@ __global__ __launch_bounds__(64 * NW) void conv_split_ws_kernel(const float* __r
                     for (int k = 1; k < KS; ++k) {
                         const int other = co_sub + 2 * ((kp + k) % KS + KS * pp);
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) acc[q][r] += red[((other * TPW + q) * 16 + r) * 64 + lane];
+                        for (int r = 0; r < 16; ++r)
+                            acc[q][r] += red[((other * RS + (RS == 1 ? 0 : q)) * 16 + r) * 64 + lane];
                     }
         }
         const int64_t b = item / chunks;
@@ -422,7 +425,8 @@ __global__ __launch_bounds__(64 * NW) void conv_split_ws_kernel(const float* __r
 static size_t ws_lds_bytes(int ng, int Q, int ks, int nw, int dil) {
     const size_t slabs = (size_t)2 * 2 * (64 * Q + 6 * dil) * (16 * ng + 8) * 2;
     const int tpw = 2 * Q / (nw / 2 / ks);
-    return slabs + (ks > 1 ? (size_t)nw * tpw * 16 * 64 * 4 : 0);
+    const int rs = (ks == 2 && tpw == 2) ? 1 : tpw;
+    return slabs + (ks > 1 ? (size_t)nw * rs * 16 * 64 * 4 : 0);
 }
 
 // ------------------------------------------------------------------------------ FC GEMM
@@ -587,22 +591,28 @@ __global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__
     }
 }
 
-// fp16x3 FC GEMM with a 128 x 128 block tile (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from N = 128): four
-// waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA tiles, so an A fragment pair feeds two tiles and a B pair two -- 16
-// ds_read_b128 per 24 MFMAs of a 32-wide K block instead of 4 per 6 -- and each X / W element staged in LDS is read by
-// 4 tiles instead of 2.  At one workgroup per CU a K block's MFMAs (~770 cycles) are shorter than an HBM round trip,
-// so the loads run FD = 3 K blocks ahead through a register ring, split / stored into the other LDS buffer one block
-// ahead.  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2): the column tiles of one row
+// fp16x3 FC GEMM with a 128 x 128 block tile (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from N = 128), each
+// X / W element staged in LDS read by 4 MFMA tiles instead of the 64 x 64 kernel's 2.  WM x WN waves: 2 x 2 (64 x 64
+// per wave, 16 ds_read_b128 per 24 MFMAs of a 32-wide K block; used) or 2 x 4 (64 x 32 per wave, two waves per
+// SIMD): measured equal, 408 vs 414 us average over FC0-FC2 per 4096 codewords (profiles/round4/conv_kernel_stats*.csv).  At one workgroup per CU a K block's MFMAs (~770 SIMD cycles) are shorter than an HBM round trip, so the loads
+// run FD = 3 K blocks ahead through a register ring, split / stored into the other LDS buffer one block ahead.  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2): the column tiles of one row
 // block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords -- is read from HBM once, not once per
 // column tile.  LDS 80 KB (dynamic).
 constexpr int FB = 128;
 constexpr int FD = 3;
 constexpr size_t kFcBigLds = (size_t)2 * 4 * FB * GS16 * 2;
 
-__global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Whi,
-                                                           const uint16_t* __restrict__ Wlo,
-                                                           const float* __restrict__ bias, float* __restrict__ out,
-                                                           int M, int K, int Nout, int act, float descale) {
+// WM x WN waves over the 128 x 128 tile, each (128 / WM) x (128 / WN) = TM x TN MFMA tiles of 32 x 32
+template <int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float* __restrict__ X,
+                                                                    const uint16_t* __restrict__ Whi,
+                                                                    const uint16_t* __restrict__ Wlo,
+                                                                    const float* __restrict__ bias,
+                                                                    float* __restrict__ out, int M, int K, int Nout,
+                                                                    int act, float descale) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = FB / 32 / WM, TN = FB / 32 / WN;
+    constexpr int UA = 1024 / NT, UB = 512 / NT;  // f4 loads per thread: A (128 x 32 fp32), each B plane
     extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [buf][plane A hi, A lo, B hi, B lo][128][GS16]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -613,22 +623,21 @@ __global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restri
     int lin = blockIdx.x;
     if ((total & 7) == 0) lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
     const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
-    const int wm = wave & 1, wn = wave >> 1;
+    const int wm = wave % WM, wn = wave / WM;
     constexpr int PL = FB * GS16;  // halfs per plane
-    // loader: A 128 rows x 32 k fp32 = 1024 f4 (4 per thread); B planes 128 x 32 fp16 = 512 x 16 B (2 per thread each)
-    f4 ra[FD][4], rbh[FD][2], rbl[FD][2];
+    f4 ra[FD][UA], rbh[FD][UB], rbl[FD][UB];
     auto fetch = [&](int slot, int k0) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int idx = tid + 256 * u;
+        for (int u = 0; u < UA; ++u) {
+            const int idx = tid + NT * u;
             const int r = idx >> 3, c4 = (idx & 7) * 4;
             int mr = m0 + r;
             if (mr >= M) mr = M - 1;
             ra[slot][u] = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int idx = tid + 256 * u;
+        for (int u = 0; u < UB; ++u) {
+            const int idx = tid + NT * u;
             const int r = idx >> 2, c8 = (idx & 3) * 8;
             rbh[slot][u] = *reinterpret_cast<const f4*>(Whi + (int64_t)(j0 + r) * K + k0 + c8);
             rbl[slot][u] = *reinterpret_cast<const f4*>(Wlo + (int64_t)(j0 + r) * K + k0 + c8);
@@ -637,8 +646,8 @@ __global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restri
     auto stash = [&](int slot, int buf) {
         _Float16* const base = smb + (size_t)buf * 4 * PL;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int idx = tid + 256 * u;
+        for (int u = 0; u < UA; ++u) {
+            const int idx = tid + NT * u;
             const int r = idx >> 3, c4 = (idx & 7) * 4;
             hf4 hi, lo;
 #pragma unroll
@@ -651,21 +660,21 @@ __global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restri
             *reinterpret_cast<hf4*>(base + PL + r * GS16 + c4) = lo;
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int idx = tid + 256 * u;
+        for (int u = 0; u < UB; ++u) {
+            const int idx = tid + NT * u;
             const int r = idx >> 2, c8 = (idx & 3) * 8;
             *reinterpret_cast<f4*>(base + 2 * PL + r * GS16 + c8) = rbh[slot][u];
             *reinterpret_cast<f4*>(base + 3 * PL + r * GS16 + c8) = rbl[slot][u];
         }
     };
-    f16v acc[2][2];
+    f16v acc[TM][TN];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < TN; ++b)
             acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int nk = K / GK;
-    const int ar = (wm * 64 + col) * GS16 + 8 * h, br = (wn * 64 + col) * GS16 + 8 * h;
+    const int ar = (wm * 32 * TM + col) * GS16 + 8 * h, br = (wn * 32 * TN + col) * GS16 + 8 * h;
     // K block kb lives in ring slot kb % FD until it is stashed into LDS buffer kb & 1
     fetch(0, 0);
 #pragma unroll
@@ -679,18 +688,21 @@ __global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restri
         if (kb + FD < nk) fetch(SL, (kb + FD) * GK);  // slot SL was stashed at step kb - 1
 #pragma unroll
         for (int st = 0; st < GK / 16; ++st) {
-            hf8 ah[2], al[2], bh[2], bl[2];
+            hf8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < TM; ++t) {
                 ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GS16 + 16 * st);
                 al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GS16 + 16 * st);
+            }
+#pragma unroll
+            for (int t = 0; t < TN; ++t) {
                 bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GS16 + 16 * st);
                 bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GS16 + 16 * st);
             }
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b) {
+                for (int b = 0; b < TN; ++b) {
                     acc[a][b] = mfma16(ah[a], bh[b], acc[a][b]);
                     acc[a][b] = mfma16(ah[a], bl[b], acc[a][b]);
                     acc[a][b] = mfma16(al[a], bh[b], acc[a][b]);
@@ -708,14 +720,14 @@ __global__ __launch_bounds__(256) void fc_split_big_kernel(const float* __restri
     if (kb < nk) step(kb, std::integral_constant<int, 0>{});
     if (kb + 1 < nk) step(kb + 1, std::integral_constant<int, 1>{});
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int j = j0 + wn * 64 + 32 * b + col;
+        for (int b = 0; b < TN; ++b) {
+            const int j = j0 + wn * 32 * TN + 32 * b + col;
             const float bj = bias[j];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * 64 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int m = m0 + wm * 32 * TM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < M) {
                     float v = fmaf(acc[a][b][r], descale, bj);
                     if (act) v = gelu(v);
@@ -1004,12 +1016,12 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
-        NPD_HIP(hipFuncSetAttribute((const void*)fc_split_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        NPD_HIP(hipFuncSetAttribute((const void*)fc_split_big_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kFcBigLds));
-        const void* ws[9] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
+        const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
                               (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
                               (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
-                              (const void*)conv_split_ws_kernel<4, 1, 2, 8>, (const void*)conv_split_ws_kernel<4, 2, 2, 8>,
+                              (const void*)conv_split_ws_kernel<4, 1, 2, 4>,
                               (const void*)conv_split_ws_kernel<8, 1, 4, 8>};
         for (const void* k : ws) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
@@ -1044,11 +1056,13 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 // spills) run the slab kernel below.
                 const int ng = (L.cin + 15) / 16;
                 const int ks = ng <= 3 ? 1 : (ng == 8 ? 4 : 2);  // ng in {1, 2, 3, 4, 8}
-                const int nw = ng <= 3 ? 4 : 8;
-                const int Q = (ng <= 4 && N % 128 == 0) ? 2 : 1;
+                const int nw = ng == 8 ? 8 : 4;
+                const int Q = (ng <= 3 && N % 128 == 0) ? 2 : 1;
                 const int nslices = (L.cout + 63) / 64;
                 const int64_t items = nb * (N / (64 * Q)) * nslices;
-                int64_t nblk = device_cu_count();
+                // cin 64: two independent 4-wave blocks per CU (67 KB of LDS each), so one block's barrier and
+                // latency waits are filled by the other's work; the others one 8- or 4-wave block per CU
+                int64_t nblk = (int64_t)device_cu_count() * (ng == 4 ? 2 : 1);
                 nblk -= nblk % nslices;
                 if (nblk > items) nblk = items;
                 if (nblk < nslices) nblk = nslices;
@@ -1058,7 +1072,7 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
     hipLaunchKernelGGL((conv_split_ws_kernel<NGV, QV, KSV, NWV>), dim3((unsigned)nblk), dim3(64 * NWV), ls, s, in, o, \
                        rsrc, wi, c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, L.descale, nb, nslices)
                 if (ng == 8) NPD_WS(8, 1, 4, 8);
-                else if (ng == 4) { if (Q == 2) NPD_WS(4, 2, 2, 8); else NPD_WS(4, 1, 2, 8); }
+                else if (ng == 4) NPD_WS(4, 1, 2, 4);
                 else if (ng == 1) { if (Q == 2) NPD_WS(1, 2, 1, 4); else NPD_WS(1, 1, 1, 4); }
                 else if (ng == 2) { if (Q == 2) NPD_WS(2, 2, 1, 4); else NPD_WS(2, 1, 1, 4); }
                 else { if (Q == 2) NPD_WS(3, 2, 1, 4); else NPD_WS(3, 1, 1, 4); }
@@ -1110,7 +1124,7 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 const uint16_t* wl = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][1]);
                 if (fo[f] % FB == 0) {
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    hipLaunchKernelGGL(fc_split_big_kernel, gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,
+                    hipLaunchKernelGGL((fc_split_big_kernel<2, 2>), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_descale[f]);
                 } else {
                     hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
