@@ -597,10 +597,15 @@ __global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__
 // SIMD): measured equal, 408 vs 414 us average over FC0-FC2 per 4096 codewords (profiles/round4/conv_kernel_stats*.csv).  At one workgroup per CU a K block's MFMAs (~770 SIMD cycles) are shorter than an HBM round trip, so the loads
 // run FD = 3 K blocks ahead through a register ring, split / stored into the other LDS buffer one block ahead.  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2): the column tiles of one row
 // block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords -- is read from HBM once, not once per
-// column tile.  LDS 80 KB (dynamic).
+// column tile.  LDS 144 KB (dynamic).
 constexpr int FB = 128;
 constexpr int FD = 3;
-constexpr size_t kFcBigLds = (size_t)2 * 4 * FB * GS16 * 2;
+// LDS row stride of the 128-row planes: 72 halfs (144 B = 36 banks, as the conv slabs) -- the 64 x 64 kernel's 40
+// (80 B = 20 banks) left a third of this kernel's LDS cycles bank-conflicted (PMC SQ_LDS_BANK_CONFLICT /
+// SQ_LDS_IDX_ACTIVE, profiles/round4/pmc_conv_summary.json); removing them moved the kernel by 2 % (405 vs 408-414 us
+// average per 4096 codewords, conv_kernel_stats_v4.csv): the conflicts were not its limit
+constexpr int GSB = 72;
+constexpr size_t kFcBigLds = (size_t)2 * 4 * FB * GSB * 2;
 
 // WM x WN waves over the 128 x 128 tile, each (128 / WM) x (128 / WN) = TM x TN MFMA tiles of 32 x 32
 template <int WM, int WN>
@@ -613,7 +618,7 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = FB / 32 / WM, TN = FB / 32 / WN;
     constexpr int UA = 1024 / NT, UB = 512 / NT;  // f4 loads per thread: A (128 x 32 fp32), each B plane
-    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [buf][plane A hi, A lo, B hi, B lo][128][GS16]
+    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [buf][plane A hi, A lo, B hi, B lo][128][GSB]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -624,7 +629,7 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
     if ((total & 7) == 0) lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
     const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
     const int wm = wave % WM, wn = wave / WM;
-    constexpr int PL = FB * GS16;  // halfs per plane
+    constexpr int PL = FB * GSB;  // halfs per plane
     f4 ra[FD][UA], rbh[FD][UB], rbl[FD][UB];
     auto fetch = [&](int slot, int k0) {
 #pragma unroll
@@ -656,15 +661,15 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
                 hi[e] = (_Float16)x;
                 lo[e] = (_Float16)(x - (float)hi[e]);
             }
-            *reinterpret_cast<hf4*>(base + r * GS16 + c4) = hi;
-            *reinterpret_cast<hf4*>(base + PL + r * GS16 + c4) = lo;
+            *reinterpret_cast<hf4*>(base + r * GSB + c4) = hi;
+            *reinterpret_cast<hf4*>(base + PL + r * GSB + c4) = lo;
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const int idx = tid + NT * u;
             const int r = idx >> 2, c8 = (idx & 3) * 8;
-            *reinterpret_cast<f4*>(base + 2 * PL + r * GS16 + c8) = rbh[slot][u];
-            *reinterpret_cast<f4*>(base + 3 * PL + r * GS16 + c8) = rbl[slot][u];
+            *reinterpret_cast<f4*>(base + 2 * PL + r * GSB + c8) = rbh[slot][u];
+            *reinterpret_cast<f4*>(base + 3 * PL + r * GSB + c8) = rbl[slot][u];
         }
     };
     f16v acc[TM][TN];
@@ -674,7 +679,7 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
         for (int b = 0; b < TN; ++b)
             acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int nk = K / GK;
-    const int ar = (wm * 32 * TM + col) * GS16 + 8 * h, br = (wn * 32 * TN + col) * GS16 + 8 * h;
+    const int ar = (wm * 32 * TM + col) * GSB + 8 * h, br = (wn * 32 * TN + col) * GSB + 8 * h;
     // K block kb lives in ring slot kb % FD until it is stashed into LDS buffer kb & 1
     fetch(0, 0);
 #pragma unroll
@@ -691,13 +696,13 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
             hf8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
             for (int t = 0; t < TM; ++t) {
-                ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GS16 + 16 * st);
-                al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GS16 + 16 * st);
+                ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GSB + 16 * st);
+                al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GSB + 16 * st);
             }
 #pragma unroll
             for (int t = 0; t < TN; ++t) {
-                bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GS16 + 16 * st);
-                bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GS16 + 16 * st);
+                bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GSB + 16 * st);
+                bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GSB + 16 * st);
             }
 #pragma unroll
             for (int a = 0; a < TM; ++a)
