@@ -121,18 +121,21 @@ def code_from_args(args):
 
 
 def rnn_from_checkpoint(ckpt, device="cuda", precision="fp32"):
-    """(net, RNN_decoder, code) of a CRISP GRU checkpoint ({'net', 'args'}, rnn_all.py:1310-1330);
-    decoding_type y_input without the y-MLP (the path the fused kernel runs)."""
+    """(net, RNN_decoder, code) of a CRISP checkpoint ({'net', 'args'}, rnn_all.py:1310-1330): decoding_type y_input
+    without the y-MLP (the CRISP scripts) or y_h0 with it (rnn_all.py:1316-1317), GRU or LSTM cells."""
     from .rnn import RNN_Model, RNN_decoder
     if isinstance(ckpt, str):
         ckpt = load_checkpoint(ckpt)
     a = ckpt["args"]
-    if getattr(a, "decoding_type", "y_input") != "y_input" or getattr(a, "use_ynn", False):
-        raise NotImplementedError("fused GRU decode supports decoding_type 'y_input' without --use_ynn")
+    dtype = getattr(a, "decoding_type", "y_input")
+    if dtype not in ("y_input", "y_h0") or (dtype == "y_input" and getattr(a, "use_ynn", False)):
+        raise NotImplementedError("fused decode supports decoding_type 'y_input' without --use_ynn, and 'y_h0'")
     onehot = bool(getattr(a, "onehot", False))
     N = int(a.N)
-    net = RNN_Model(getattr(a, "rnn_type", "GRU"), N + 1 + int(onehot), int(a.rnn_feature_size), 1, int(a.rnn_depth), N,
-                    0, 0, getattr(a, "activation", "selu"), float(getattr(a, "dropout", 0.0)),
+    din = (N if dtype == "y_input" else 0) + 1 + int(onehot)
+    yh, yd = (0, 0) if dtype == "y_input" else (int(getattr(a, "y_hidden_size", 128)), int(getattr(a, "y_depth", 3)))
+    net = RNN_Model(getattr(a, "rnn_type", "GRU"), din, int(a.rnn_feature_size), 1, int(a.rnn_depth), N,
+                    yh, yd, getattr(a, "activation", "selu"), float(getattr(a, "dropout", 0.0)),
                     bool(getattr(a, "use_skip", False)), out_linear_depth=int(getattr(a, "out_linear_depth", 1)),
                     bidirectional=bool(getattr(a, "bidirectional", False)),
                     use_layernorm=bool(getattr(a, "use_layernorm", False))).to(device)
@@ -141,7 +144,7 @@ def rnn_from_checkpoint(ckpt, device="cuda", precision="fp32"):
     code = code_from_args(a)
     info = getattr(code, "info_positions", None)
     info = np.asarray(info if info is not None else code.B)
-    dec = RNN_decoder("y_input", N, info, onehot=onehot, reverse_order=bool(getattr(a, "reverse_order", False)),
+    dec = RNN_decoder(dtype, N, info, onehot=onehot, reverse_order=bool(getattr(a, "reverse_order", False)),
                       precision=precision)
     return net, dec, code
 

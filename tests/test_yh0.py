@@ -52,3 +52,21 @@ def test_rnn_model_get_h0_matches_reference(name):
         h0 = net.get_h0(torch.from_numpy(d["y"]))
     x = h0.permute(1, 2, 0).reshape(d["y"].shape[0], -1).numpy()
     assert np.abs(x - d["h0x"]).max() < 1e-6
+
+
+def test_rnn_from_checkpoint_y_h0():
+    """A y_h0 checkpoint in the reference's format ({'net': state_dict, 'args': Namespace}, rnn_all.py:1310-1330)
+    loads with its y-MLP through datasets.rnn_from_checkpoint and reproduces the reference's initial states."""
+    import argparse
+    from neural_polar_decoder_amd.datasets import rnn_from_checkpoint
+    d, sd = load("gru_yh0_polar_64_32")
+    args = argparse.Namespace(decoding_type="y_h0", onehot=True, N=64, K=32, rnn_feature_size=64, rnn_depth=2,
+                              y_hidden_size=int(d["y_hidden"]), y_depth=int(d["y_depth"]), activation="selu",
+                              code="Polar", rate_profile="polar", target_K=32, rnn_type="GRU")
+    net, dec, code = rnn_from_checkpoint({"net": {k: torch.from_numpy(v) for k, v in sd.items()}, "args": args},
+                                         device="cpu")
+    assert dec.decoding_type == "y_h0" and net.fused_supported("y_h0")
+    assert np.array_equal(np.asarray(code.info_positions), d["info"])
+    with torch.no_grad():
+        h0 = net.get_h0(torch.from_numpy(d["y"]))
+    assert np.abs(h0.permute(1, 2, 0).reshape(d["y"].shape[0], -1).numpy() - d["h0x"]).max() < 1e-6
