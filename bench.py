@@ -1,35 +1,32 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Polar(64,32) SC decoding on MI355X (BASELINE.json configs[1]), plus the other
-configs' legs and the combined SC + CRISP-GRU eval step the metric string names.
+"""Headline benchmark: the metric BASELINE.json names -- codewords/s of the Polar(64,32) SC + CRISP-GRU eval step
+(rnn_all.py:853-880: SC and the CRISP GRU decode the same received words at every SNR point, both counted).
 
-``value`` -- one "step" = SC-decode one batch of B = 2^20 received words per SNR point for the SNR
-sweep 0,1,2,3,4 dB per GPU (one launch of the fused decode + BER/BLER-count kernel; y resident in
-HBM before timing, msg_hat (B,K) fp32 written back, error counters accumulated on device).
+``value`` -- one "step" = for the SNR sweep 0,1,2,3,4 dB, B = 2^20 received words per SNR point per GPU (resident in
+HBM before timing): one SC launch over the whole sweep (npd_sc_decode_mc_sweep: decode + fused BER/BLER counts,
+msg_hat written) and, per SNR point, one CRISP GRU decode (hidden 64, 2 layers, onehot y_input; the trained
+tests/golden/trained_crisp_64_32.npz weights; fp16x3 split MFMA kernel gru16p_kernel, fp32 accumulation) plus its
+device error count.  K steps are timed between barrier + synchronize; HIP events on the launch stream time every SC
+and GRU launch inside the timed region (the roofline's launch durations).
 
-Secondary legs (same JSON line; every leg runs on every rank over its own codeword shard, is timed
-between barriers and reports the max over ranks; whole-job codewords/s):
-  montecarlo      the Monte-Carlo step itself: Philox message -> encode -> AWGN -> SC -> count, all
-                  SNR points, y never stored (fused kernel)
-  metric_as_named the metric as named (top-level record): the eval step of rnn_all.py:853-880 on the same
-                  words -- SC and CRISP GRU (hidden 64, 2 layers; trained with the reference's loop) both decode
-                  every word of the sweep (configs[1]+[2]); its own roofline (GRU kernel, fp32 MFMA) and
-                  cpu_baseline (oracle SC + GRU on the host cores)
-  crisp_gru       configs[2]: GRU decode alone, B = 2^20, fp32 (plus opt-in bf16x3 / bf16 kernels)
-  pac_gru         configs[3]: PAC(128,64) CRISP GRU, 2^20 codewords per GPU (2^23 at 8 GPUs), RCCL
-                  all-reduce of the BER/BLER counters
-  pac_sc          PAC(128,64) SC decoding (the configs[3] eval's SC baseline, rnn_all.py:696)
-  conv_model      configs[4]: Polar(256,128) convNet (embed 128), fp16x3 split MFMA (fp32 MFMA path beside)
-  scl             SC-List L = 4, 8 at Polar(64,32) and L = 4 at Polar(256,128) (run_models.py:329)
-  sc_lse          exact-LSE SC (polar.py:209-279)
+Other configurations run as sub-records (same weak-scaling rules; every leg decodes its own codeword shard per rank,
+timed between barriers, max over ranks; whole-job codewords/s):
+  configs1_sc     configs[1]: SC decode alone (the SC half of the step, HBM-bound) + its PMC traffic
+  montecarlo      the fused Monte-Carlo step: Philox message -> encode -> AWGN -> SC -> count, y never stored
+  crisp_gru       configs[2]: GRU decode alone, fp32 kernel (the reference's arithmetic) + split-MFMA kernels
+  crisp_gru_f512  run_crisp.sh's decoder width (hidden 512, weight-streaming kernel)
+  pac_gru/pac_sc  configs[3]: PAC(128,64) CRISP GRU and PAC SC, RCCL all-reduce of the counters
+  conv_model      configs[4]: Polar(256,128) convNet (embed 128), fp16x3 split MFMA (fp32 path beside)
+  scl, sc_lse     SC-List (run_models.py:329) and exact-LSE SC (polar.py:209-279)
 
   python bench.py [--gpus N --steps K --warmup W]
   --gpus N > 1 without a launcher: bench.py starts `python -m torch.distributed.run --nproc-per-node N`
   on itself (the parent never touches the GPU) and exits with its status.  Under a launcher,
   WORLD_SIZE must equal --gpus.
 
-Prints ONE JSON line (rank 0).  The roofline leg times every decode launch with HIP events on the
-stream the kernel runs on; the cpu_baseline leg times the CPU oracle (oracle/, a bit-exact C
-restatement of the reference's sc_decode_new) on a bounded sample of the same received words.
+Rank 0 writes the full record (every leg) to --full-json and prints ONE compact JSON line last (the headline, its
+roofline and cpu_baseline, and one summary per configuration).  cpu_baseline times the CPU oracle (oracle/: C
+restatements of sc_decode_new and RNN_decoder.decode) on a bounded sample of the same received words.
 """
 from __future__ import annotations
 
@@ -142,13 +139,15 @@ def parse():
     ap.add_argument("--snrs", type=str, default="0,1,2,3,4")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gru", action="store_true", help="skip the GRU legs (metric_as_named, crisp_gru, pac_gru)")
+    ap.add_argument("--no-gru", action="store_true", help="skip the GRU legs besides the headline (fp32 path, crisp_gru, crisp_gru_f512, pac_gru)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--no-conv", action="store_true", help="skip the conv-model leg")
     ap.add_argument("--no-scl", action="store_true", help="skip the SC-List leg")
     ap.add_argument("--no-lse", action="store_true", help="skip the exact-LSE SC leg")
     ap.add_argument("--no-mc", action="store_true", help="skip the fused Monte-Carlo leg")
     ap.add_argument("--no-pac", action="store_true", help="skip the PAC(128,64) SC leg")
+    ap.add_argument("--full-json", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
+                    help="where rank 0 writes the full record (every leg); the printed line is the compact summary")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # CPU test of the launcher
     return ap.parse_args()
@@ -312,91 +311,34 @@ def mc_leg(code, snrs, B, cw0, world, timer, dev, ref_counts):
 
 
 PRECISION_JSON = os.path.join(ROOT, "profiles", "round4", "gru_precision.json")
-PMC_GRU_JSON = os.path.join(ROOT, "profiles", "round4", "pmc_gru_summary.json")
 
 
-def split_issue_bound(ms16, B, steps):
-    """Combined MFMA + VALU issue bound of gru16p_kernel from its committed PMC (profiles/round4/pmc_gru_summary.json):
-    the two serialise on a SIMD (profiles/round3/coissue.txt), so the kernel needs at least (MFMA busy + VALU busy)
-    cycles per SIMD.  Per wave-step cycles from the counters, scaled to this launch, over the clock the chip held in
-    the PMC run (GRBM_GUI_ACTIVE / 8 / kernel time) and over the 2.4 GHz the spec peaks assume; frac = ceiling time /
-    this launch's time (above 1 at the PMC run's clock when this run holds a higher one)."""
-    if not os.path.exists(PMC_GRU_JSON):
-        return None
-    pm = json.load(open(PMC_GRU_JSON))
-    k = next((v for n, v in pm.items() if "gru16p_kernel" in n and isinstance(v, dict)), None)
-    if not k or "per_wave_step" not in k:
-        return None
-    ws = k["per_wave_step"]  # mfma_cycles, valu_cycles per 16-codeword wave and decoding step
-    simds = 1024
-    # each v_mfma_f32_16x16x32_f16 (16 busy cycles) also holds vector issue for 4 of the cycles SQ_ACTIVE_INST_VALU
-    # counts, so those are in both counters once: serialised cycles = MFMA busy + VALU active - 4 x MFMA count
-    serial = ws["mfma_cycles"] + ws["valu_cycles"] - 4.0 * ws["mfma_cycles"] / 16.0
-    cycles = serial * (B / 16) * steps / simds
-    at_held = cycles / (k["clock_ghz"] * 1e9) * 1e3
-    at_spec = cycles / 2.4e9 * 1e3
-    return {"bound": "mfma + valu issue (serialised on the SIMD)", "pmc": "profiles/round4/pmc_gru_summary.json",
-            "mfma_cycles_per_wave_step": ws["mfma_cycles"], "valu_cycles_per_wave_step": ws["valu_cycles"],
-            "serialised_cycles_per_wave_step": serial,
-            "ceiling_ms_at_2.4GHz": at_spec, "ceiling_ms_at_held_clock": at_held, "held_clock_ghz": k["clock_ghz"],
-            "frac_at_2.4GHz": at_spec / ms16, "frac_at_held_clock": at_held / ms16}
-
-
-def sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
-    """The eval step the metric names (rnn_all.py:853-880): SC and the CRISP GRU decode the same words at every
-    SNR point and both are counted.  The GRU runs on the fp16x3 split kernel: its logit error against a float64
-    decoder equals the fp32 kernel's (profiles/round4/gru_precision.json, enforced by tests/test_gru_precision_gpu.py);
-    the fp32 kernel's step is reported beside it (fp32_path)."""
+def sc_plus_gru_fp32(code, snrs, B, cw0, world, timer, dev, yall, msg, hat):
+    """The headline step with the GRU on the fp32 kernel (gru_decode_kernel<64,2>, the reference's arithmetic):
+    the same SC launch and five GRU decodes + counts.  Reported beside the fp16x3 headline."""
     from neural_polar_decoder_amd.utils import count_errors
     c_sc = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    cg = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
-    flop_cw = gru_flop_per_cw(N_CODE, 64)
-    paths = {}
-    for prec in ("fp16x3", "fp32"):
-        net, dec, wdesc, fix = crisp_model(code, dev, precision=prec)
-        cg_dev = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    net, dec, _, _ = crisp_model(code, dev, precision="fp32")
 
-        def step():
-            code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)  # decoded_SC_msg_bits, rnn_all.py:853
-            for si in range(len(snrs)):
-                count_errors(msg, dec.decode(net, False, yall[si]), cg_dev[si], cols=code.info_positions)
+    def step():
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)
+        for si in range(len(snrs)):
+            count_errors(msg, dec.decode(net, False, yall[si]), cg[si], cols=code.info_positions)
 
-        t = timer(step, iters=2, warm=1)
-        # the GRU kernel alone, HIP events on its stream (one launch = one SNR point's 2^20 words)
-        ms = event_ms(lambda: dec.decode(net, False, yall[2]), 3, stream)
-        allreduce(cg_dev, _sum(), world)
-        paths[prec] = dict(t=t, ms=ms, cg=cg_dev.cpu().numpy() // 3, wdesc=wdesc, fix=fix)  # 3 counted passes
+    t = timer(step, iters=2, warm=1)
+    ms = event_ms(lambda: dec.decode(net, False, yall[2]), 2, stream)
+    allreduce(cg, _sum(), world)
+    cc = cg.cpu().numpy() // 3  # three counted passes
+    tf = gru_flop_per_cw(N_CODE, 64) * B / (ms / 1e3) / 1e12
     n = world * B
-    p16, p32 = paths["fp16x3"], paths["fp32"]
-    tf16 = flop_cw * B / (p16["ms"] / 1e3) / 1e12
-    tf32 = flop_cw * B / (p32["ms"] / 1e3) / 1e12
-    prec_table = json.load(open(PRECISION_JSON)) if os.path.exists(PRECISION_JSON) else None
-    cg = p16["cg"]
-    return {"value": world * len(snrs) * B / p16["t"], "unit": "codewords/s (each decoded by SC and by the GRU)",
-            "ms_per_step": p16["t"] * 1e3, "weights": p16["wdesc"],
-            "gru_precision": "fp16x3: hi + lo fp16 split, 3 v_mfma_f32_16x16x32_f16 products per multiply, fp32 "
-                             "accumulation (gru16p_kernel); logit error vs a float64 decoder equal to the fp32 kernel's",
-            "precision_evidence": None if prec_table is None else {
-                "source": "profiles/round4/gru_precision.json (tools/gru_precision.py)",
-                "abs_logit_error_vs_float64": {k: {q: v[q] for q in ("p50", "p99", "p99.9", "max", "cw_flips")}
-                                               for k, v in prec_table["impls"].items()},
-                "words": prec_table["words"]},
-            "roofline": dict({"kernel": "gru16p_kernel<5> (16-codeword waves, fp16x3)", "achieved": tf16,
-                              "unit": "TFLOP/s", "peak_fp16_dense": 2516.6, "frac_of_fp16_peak": tf16 / 2516.6,
-                              "algorithmic_flop_per_cw": flop_cw, "codewords_per_launch": B,
-                              "avg_launch_ms": p16["ms"]}, **(split_issue_bound(p16["ms"], B, N_CODE) or {})),
-            "gru_ber": {str(s): float(cg[i, 0]) / (n * K_CODE) for i, s in enumerate(snrs)},
-            "gru_bler": {str(s): float(cg[i, 1]) / n for i, s in enumerate(snrs)},
-            "gru_vs_reference": gru_vs_reference(p16["fix"], snrs, cg[:, 0], cg[:, 1], n, K_CODE),
-            "gru_errors_fp32_minus_fp16x3": {"bits": [int(a) - int(b) for a, b in zip(p32["cg"][:, 0], cg[:, 0])],
-                                             "blocks": [int(a) - int(b) for a, b in zip(p32["cg"][:, 1], cg[:, 1])]},
-            "fp32_path": {"value": world * len(snrs) * B / p32["t"], "ms_per_step": p32["t"] * 1e3,
-                          "roofline": {"bound": "mfma", "kernel": "gru_decode_kernel<64,2> (fp32 v_mfma_f32_32x32x2_f32)",
-                                       "achieved": tf32, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
-                                       "frac": tf32 / FP32_PEAK_TF, "avg_launch_ms": p32["ms"]},
-                          "gru_ber": {str(s): float(p32["cg"][i, 0]) / (n * K_CODE) for i, s in enumerate(snrs)}},
-            "config": "configs[1]+[2]: Polar(64,32), 2^20 words per SNR per GPU, 0-4 dB; SC sweep launch + 5 CRISP "
-                      "GRU (hidden 64, 2 layers) decodes + device counts"}
+    return {"value": world * len(snrs) * B / t, "ms_per_step": t * 1e3,
+            "roofline": {"bound": "mfma", "kernel": "gru_decode_kernel<64,2> (fp32 v_mfma_f32_32x32x2_f32)",
+                         "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "frac": tf / FP32_PEAK_TF,
+                         "avg_launch_ms": ms},
+            "gru_ber": {str(s_): float(cc[i, 0]) / (n * K_CODE) for i, s_ in enumerate(snrs)},
+            "gru_bler": {str(s_): float(cc[i, 1]) / n for i, s_ in enumerate(snrs)}}
 
 
 def cpu_baseline_sc_gru(yall_host, snrs, info, net, budget_s):
@@ -453,7 +395,8 @@ def gru_leg(code, dev, y, B, world, timer):
     return {"value": f["value"], "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": f["avg_launch_ms"],
             "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "algorithmic_flop_per_cw": flop_cw,
             "achieved_tflops": f["achieved_tflops"], "peak_tflops_fp32": FP32_PEAK_TF, "frac": f["frac"],
-            "fp16x3": dict(res["fp16x3"], note="scaled hi+lo fp16 split (3 products per multiply, fp32 accumulate): "
+            "fp16x3": dict(res["fp16x3"], note="unscaled hi+lo fp16 split with the gate exp2 constants folded into the "
+                                                "weights (gru16p_kernel<5>: 3 products per multiply, fp32 accumulate): "
                                                 "held to the fp32 path's tolerance in tests/test_gru_gpu.py"),
             "bf16x3": res["bf16x3"], "bf16": res["bf16"], "weights": wdesc,
             "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input, 2 dB, 2^20 per GPU"}
@@ -624,9 +567,10 @@ CONV_PRECISION_JSON = os.path.join(ROOT, "profiles", "round4", "conv_precision.j
 def conv_leg(dev, rank, world, timer, batch=8192):
     """configs[4]: Polar(256,128) convNet decoder, embed 128 (run_alt.sh), seeded random weights; batch per GPU,
     whole-job codewords/s.  The record runs the fp16x3 path (conv and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo
-    split, fp32 accumulation): its logit error against a float64 forward is below the fp32 path's at every percentile
-    (profiles/round4/conv_precision.json, tools/conv_precision.py; enforced by tests/test_conv_gpu.py); the fp32 MFMA
-    path is reported beside it (fp32_path)."""
+    split, fp32 accumulation): measured, its logit error against a float64 forward is below the fp32 path's at every
+    percentile (profiles/round4/conv_precision.json, tools/conv_precision.py); tests/test_conv_gpu.py enforces the looser
+    bound of 1.5x the fp32 path's error at p50 / p99 / p99.9 and 2x at the maximum; the fp32 MFMA path is reported beside
+    it (fp32_path)."""
     from neural_polar_decoder_amd import reference_polar_code
     from neural_polar_decoder_amd.montecarlo import seeded_conv
     net = seeded_conv(256, 128, seed=0, device=dev)
@@ -725,6 +669,11 @@ def traffic_child(args):
     cnt = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
     for _ in range(4):
         code.sc_decode_mc_sweep(yall, snrs, SEED, 0, cnt, msg_hat=hat)
+    # the headline's GRU launches: fp16x3 CRISP GRU on one SNR point's 2^20 words
+    net, dec, _, _ = crisp_model(code, dev, precision="fp16x3")
+    for _ in range(4):
+        dec.decode(net, False, yall[2])
+    torch.cuda.synchronize()
     del yall, hat
     # the pac_sc leg's launch: PAC(128,64) streaming SC + counts + msg_hat, 2^20 words at 2 dB
     import argparse as _ap
@@ -738,12 +687,13 @@ def traffic_child(args):
 
 
 PAC_KERNEL = "sc_decode_kernel<128"
+GRU_KERNEL = "gru16p_kernel"
 
 
 def pmc_traffic(args, timeout_s=240):
-    """HBM bytes per launch of the headline decode kernel and of the pac_sc leg's kernel, from rocprofv3 PMC
-    counters, one counter per pass (MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of wide coalesced
-    streaming reads on gfx950 -> doubled; WRITE_SIZE exact for 16-B/lane streaming stores; both in KiB).
+    """HBM bytes per launch of the SC decode kernel, the headline's GRU kernel and the pac_sc leg's kernel, from
+    rocprofv3 PMC counters, one counter per pass (MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of wide
+    coalesced streaming reads on gfx950 -> doubled; WRITE_SIZE exact for 16-B/lane streaming stores; both in KiB).
     Returns ({kernel prefix: bytes per launch}, how)."""
     import csv
     import glob
@@ -751,8 +701,8 @@ def pmc_traffic(args, timeout_s=240):
     import tempfile
     prof = shutil.which("rocprofv3")
     if prof is None:
-        return None, "rocprofv3 not found"
-    names = (KERNEL_NAME.split("<")[0], PAC_KERNEL)
+        return None, "rocprofv3 not found", None
+    names = (KERNEL_NAME.split("<")[0], PAC_KERNEL, GRU_KERNEL)
     vals = {k: {} for k in names}
     tmp = tempfile.mkdtemp(prefix="npd_pmc_")
     env = dict(os.environ, TMPDIR="/tmp")
@@ -763,22 +713,69 @@ def pmc_traffic(args, timeout_s=240):
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env, cwd=ROOT)
         except Exception as e:  # noqa: BLE001
-            return None, f"rocprofv3 failed: {e}"
+            return None, f"rocprofv3 failed: {e}", None
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
-            return None, f"rocprofv3 rc={r.returncode}"
+            return None, f"rocprofv3 rc={r.returncode}", None
         rows = list(csv.DictReader(open(files[0])))
         for k in names:
             xs = [float(row["Counter_Value"]) for row in rows if k in row["Kernel_Name"] and row["Counter_Name"] == ctr]
             if not xs:
-                return None, f"kernel {k} not found in PMC output"
+                return None, f"kernel {k} not found in PMC output", None
             vals[k][ctr] = sum(xs[1:]) / max(1, len(xs) - 1) if len(xs) > 1 else xs[0]  # skip the first (cold) launch
     shutil.rmtree(tmp, ignore_errors=True)
     return ({k: (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024 for k, v in vals.items()},
-            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 read), one pass each")
+            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 read), one pass each",
+            {k: {c: v[c] * 1024 for c in v} for k, v in vals.items()})
 
 
 # ------------------------------------------------------------------------------------ main
+def sc_only_record(code, snrs, B, cw0, world, dev, yall, hat, steps, warmup):
+    """configs[1]: the SC half of the step alone -- one npd_sc_decode_mc_sweep launch per step (decode + fused counts
+    + msg_hat) over the resident sweep; K steps between barriers, HIP events per launch (HBM roofline)."""
+    counters = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, counters, msg_hat=hat)
+    counters.zero_()
+    ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, counters, msg_hat=hat)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    el = float(allreduce(torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev), _max(), world))
+    launch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    per_step_counts = (counters // steps).cpu()
+    allreduce(counters, _sum(), world)
+    cnt = counters.cpu().numpy()
+    n_cw = steps * world * B
+    bler = [float(cnt[i, 1]) / n_cw for i in range(len(snrs))]
+    achieved = BYTES_PER_CW * B * len(snrs) / (launch_ms / 1e3) / 1e9
+    rec = {"value": world * steps * len(snrs) * B / el, "unit": "codewords/s", "ms_per_step": el / steps * 1e3,
+           "roofline": {"bound": "hbm", "kernel": KERNEL_NAME + " (npd_sc_decode_mc_sweep: all SNR points in one launch)",
+                        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                        "traffic": None, "algorithmic_bytes_per_launch": BYTES_PER_CW * B * len(snrs),
+                        "avg_launch_ms": launch_ms},
+           "ber": {str(s_): float(cnt[i, 0]) / (n_cw * K_CODE) for i, s_ in enumerate(snrs)},
+           "bler": {str(s_): b for s_, b in zip(snrs, bler)},
+           "config": "configs[1]: Polar(64,32) min-sum SC decode + fused BER/BLER count + msg_hat, 2^20 per SNR per GPU, "
+                     "0-4 dB, one launch per sweep"}
+    if os.path.exists(ANCHORS_NPZ):  # BER curve vs the reference's: horizontal offset of the BLER curve (+-0.05 dB)
+        an = np.load(ANCHORS_NPZ)
+        ref_bler = [int(e) / int(n) for e, n in zip(an["blk_err"], an["n"])]
+        offs = db_offsets(snrs, bler, [float(x) for x in an["snr"]], ref_bler)
+        rec["ber_db_offset"] = {str(s_): o for s_, o in zip(snrs, offs)}
+        rec["ber_match"] = all(o is not None and abs(o) <= 0.05 for o in offs)
+        rec["ber_reference"] = ("tests/golden/sc_anchors_64_32.npz: the reference's sc_decode_new, 2e5 words at 0-1 dB, "
+                                f"1e6 at 2-4 dB; this run: {B} distinct words per SNR")
+    return rec, per_step_counts
+
+
 def main():
     args = parse()
     if args.traffic_child:
@@ -795,84 +792,128 @@ def main():
     world, rank, local = dist_setup()
     dev = torch.device("cuda", torch.cuda.current_device())
     from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd.utils import count_errors
 
     code = reference_polar_code(N_CODE, K_CODE)
+    info = code.info_positions
     snrs = [float(s) for s in args.snrs.split(",")]
+    nsnr = len(snrs)
     B = args.batch
     cw0 = rank * B  # weak scaling: every rank owns its own codeword range
     # the received words of every SNR point, back to back (n_snr, B, N), resident before timing
-    yall = torch.empty(len(snrs), B, N_CODE, dtype=torch.float32, device=dev)
+    yall = torch.empty(nsnr, B, N_CODE, dtype=torch.float32, device=dev)
     msg = None
     for si, snr in enumerate(snrs):
         m, _, _ = code.mc_generate(B, snr, SEED, si, cw0, want_msg=msg is None, out=yall[si])
         msg = m if msg is None else msg
-    ys = [yall[si] for si in range(len(snrs))]
-    hat = torch.empty(len(snrs), B, K_CODE, dtype=torch.float32, device=dev)
-    counters = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+    ys = [yall[si] for si in range(nsnr)]
+    hat = torch.empty(nsnr, B, K_CODE, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def step(events=None):
-        # one step = the whole SNR sweep of the batch, one launch (npd_sc_decode_mc_sweep)
-        if events is not None:
-            events[0].record(stream)
-        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, counters, msg_hat=hat)
-        if events is not None:
-            events[1].record(stream)
+    # ---------------------------------------------------------------- headline: the SC + CRISP-GRU eval step
+    net, dec, wdesc, fix = crisp_model(code, dev, precision="fp16x3")
+    dec.decode(net, False, ys[0][:64])  # weight packing + upload happen here, outside the timed region
+    c_sc = torch.zeros(nsnr, 2, dtype=torch.int64, device=dev)
+    c_gru = torch.zeros(nsnr, 2, dtype=torch.int64, device=dev)
+
+    def step(ev=None):
+        # decoded_SC_msg_bits and the RNN's decisions on the same words at every SNR point (rnn_all.py:853-880)
+        if ev is not None:
+            ev[0].record(stream)
+        code.sc_decode_mc_sweep(yall, snrs, SEED, cw0, c_sc, msg_hat=hat)
+        if ev is not None:
+            ev[1].record(stream)
+        for si in range(nsnr):
+            if ev is not None:
+                ev[2 + 2 * si].record(stream)
+            d = dec.decode(net, False, ys[si])
+            if ev is not None:
+                ev[3 + 2 * si].record(stream)
+            count_errors(msg, d, c_gru[si], cols=info)
 
     for _ in range(args.warmup):
         step()
-    counters.zero_()
+    c_sc.zero_()
+    c_gru.zero_()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2 + 2 * nsnr)] for _ in range(args.steps)]
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps)]
     barrier(world)
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(ev[k])
     torch.cuda.synchronize()
     barrier(world)
     el = time.perf_counter() - t0
-    el_t = allreduce(torch.tensor([el], dtype=torch.float64, device=dev), _max(), world)
-    elapsed = float(el_t.item())
+    elapsed = float(allreduce(torch.tensor([el], dtype=torch.float64, device=dev), _max(), world).item())
     rank_ms = [el / args.steps * 1e3]
     if world > 1:
         import torch.distributed as dist
         g = [None] * world
         dist.all_gather_object(g, el / args.steps * 1e3)
         rank_ms = g
-    launch_ms = [e[0].elapsed_time(e[1]) for e in ev]
-    avg_launch_s = float(np.mean(launch_ms)) / 1e3
-    per_step_counts = (counters // args.steps).cpu()  # the same words every step: counts scale exactly
-    allreduce(counters, _sum(), world)
-
-    total_cw = world * args.steps * len(snrs) * B
-    value = total_cw / elapsed
-    achieved = BYTES_PER_CW * B * len(snrs) / avg_launch_s / 1e9
-
-    # BER/BLER per SNR vs the reference anchors (steps x world x B codewords per SNR)
-    cnt = counters.cpu().numpy()
-    n_cw = args.steps * world * B
-    ber = {s: float(cnt[i, 0]) / (n_cw * K_CODE) for i, s in enumerate(snrs)}
-    bler = {s: float(cnt[i, 1]) / n_cw for i, s in enumerate(snrs)}
-    # BER curve vs the reference's: horizontal offset of the BLER curve in dB (north_star: within +-0.05 dB)
-    ber_db_offset, ber_match = None, None
-    if os.path.exists(ANCHORS_NPZ):
-        an = np.load(ANCHORS_NPZ)
-        ref_bler = [int(e) / int(n) for e, n in zip(an["blk_err"], an["n"])]
-        offs = db_offsets(snrs, [bler[s] for s in snrs], [float(x) for x in an["snr"]], ref_bler)
-        ber_db_offset = {str(s): o for s, o in zip(snrs, offs)}
-        ber_match = all(o is not None and abs(o) <= 0.05 for o in offs)
+    sc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    gru_ms = float(np.mean([e[2 + 2 * si].elapsed_time(e[3 + 2 * si]) for e in ev for si in range(nsnr)]))
+    allreduce(c_sc, _sum(), world)
+    allreduce(c_gru, _sum(), world)
+    csc, cg = c_sc.cpu().numpy(), c_gru.cpu().numpy()
+    n_cw = args.steps * world * B  # words counted per SNR point
+    value = world * args.steps * nsnr * B / elapsed
+    flop_cw = gru_flop_per_cw(N_CODE, 64)
+    tf16 = flop_cw * B / (gru_ms / 1e3) / 1e12
+    sc_gbs = BYTES_PER_CW * B * nsnr / (sc_ms / 1e3) / 1e9
+    gru_ber = [float(cg[i, 0]) / (n_cw * K_CODE) for i in range(nsnr)]
+    gru_bler = [float(cg[i, 1]) / n_cw for i in range(nsnr)]
+    headline = {
+        "metric": "codewords/sec Polar(64,32) SC + CRISP-GRU decode, 1/2/4/8 GPU; BER match",
+        "value": value, "unit": "codewords/s (each decoded by SC and by the CRISP GRU)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp16x3 GRU (hi + lo fp16 operands on v_mfma_f32_16x16x32_f16, fp32 accumulation and gates); fp32 SC",
+        "data": "synthetic (Philox msg -> Plotkin encode -> AWGN), resident in HBM before timing; GRU weights "
+                + wdesc,
+        "config": {"workload": "configs[1]+[2]: Polar(N=64,K=32) eval step (rnn_all.py:853-880): min-sum SC sweep launch "
+                               "+ per SNR point a CRISP GRU decode (hidden 64, 2 layers, onehot y_input) + device "
+                               "BER/BLER counts of both, 2^20 words per SNR per GPU, SNR 0-4 dB",
+                   "code": "Polar(64,32) 'polar' rate profile", "batch_per_snr_per_gpu": B, "snr_db": snrs,
+                   "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
+        "world_size_rccl": world, "rank_ms_per_step": rank_ms,
+        "roofline": {"bound": "mfma", "kernel": "gru16p_kernel<5> (fp16x3 CRISP GRU, one launch per SNR point)",
+                     "achieved": tf16, "peak": FP16_PEAK_TF, "unit": "TFLOP/s", "frac": tf16 / FP16_PEAK_TF,
+                     "traffic": None,
+                     "algorithmic": f"{flop_cw:.4g} FLOP per codeword (SURVEY.md 8(d): y.W_ih once + 64 steps of both "
+                                    f"layers' gate GEMVs + output dot) x {B} codewords per launch",
+                     "issued_frac": 3 * tf16 / FP16_PEAK_TF,
+                     "issued_note": "the split issues 3 fp16 products per multiply (hi.hi + hi.lo + lo.hi)",
+                     "avg_launch_ms": gru_ms,
+                     "sc_launch": {"bound": "hbm", "kernel": KERNEL_NAME, "achieved": sc_gbs, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": sc_gbs / HBM_PEAK_GBS, "avg_launch_ms": sc_ms,
+                                   "algorithmic_bytes_per_launch": BYTES_PER_CW * B * nsnr}},
+        "gru_ber": {str(s_): b for s_, b in zip(snrs, gru_ber)},
+        "gru_bler": {str(s_): b for s_, b in zip(snrs, gru_bler)},
+        "sc_ber": {str(s_): float(csc[i, 0]) / (n_cw * K_CODE) for i, s_ in enumerate(snrs)},
+        "sc_bler": {str(s_): float(csc[i, 1]) / n_cw for i, s_ in enumerate(snrs)},
+    }
+    gvr = gru_vs_reference(fix, snrs, cg[:, 0], cg[:, 1], n_cw, K_CODE)
+    full = {"headline": headline, "gru_vs_reference": gvr}
+    prec_table = json.load(open(PRECISION_JSON)) if os.path.exists(PRECISION_JSON) else None
+    if prec_table is not None:
+        full["gru_precision_evidence"] = {
+            "source": os.path.relpath(PRECISION_JSON, ROOT) + " (tools/gru_precision.py)",
+            "abs_logit_error_vs_float64": {k: {q: v[q] for q in ("p50", "p99", "p99.9", "max", "cw_flips")}
+                                           for k, v in prec_table["impls"].items()}, "words": prec_table["words"]}
 
     timer = Timer(world, dev)
     legs = {}
+    sc1, per_step_counts = sc_only_record(code, snrs, B, cw0, world, dev, yall, hat, args.steps, args.warmup)
+    legs["configs1_sc"] = sc1
+    if not args.no_gru:
+        legs["fp32_path"] = sc_plus_gru_fp32(code, snrs, B, cw0, world, timer, dev, yall, msg, hat)
     if not args.no_mc and hasattr(code, "sc_mc_sweep_fused"):
         ref = per_step_counts.clone()
         if world > 1:
             ref = allreduce(per_step_counts.to(dev), _sum(), world).cpu()
         legs["montecarlo"] = mc_leg(code, snrs, B, cw0, world, timer, dev, ref)
-    metric_as_named = None
     if not args.no_gru:
-        metric_as_named = sc_plus_gru_leg(code, snrs, B, cw0, world, timer, dev, yall, msg, hat)
         legs["crisp_gru"] = gru_leg(code, dev, ys[2], B, world, timer)
         legs["crisp_gru_f512"] = crisp_f512_leg(dev, rank, world, timer)
     if not (args.no_gru and args.no_pac):
@@ -886,57 +927,64 @@ def main():
 
     if rank != 0:
         return 0
-    out = {
-        "metric": "codewords/sec Polar(64,32) SC + CRISP-GRU decode, 1/2/4/8 GPU; BER match",
-        "value": value,
-        "unit": "codewords/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "fp32",
-        "data": "synthetic (Philox msg -> Plotkin encode -> AWGN), resident in HBM before timing",
-        "config": {"workload": "configs[1]: Polar(N=64,K=32) min-sum SC decode + fused BER/BLER count, "
-                               "batch 2^20 per SNR per GPU, SNR sweep 0-4 dB (the SC half of the metric; the "
-                               "SC + CRISP-GRU eval step is the metric_as_named record)",
-                   "code": "Polar(64,32) 'polar' rate profile", "batch_per_snr_per_gpu": B, "snr_db": snrs,
-                   "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
-        "world_size_rccl": world,
-        "rank_ms_per_step": rank_ms,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": KERNEL_NAME + " (npd_sc_decode_mc_sweep: all SNR points in one launch)",
-                     "algorithmic_bytes_per_launch": BYTES_PER_CW * B * len(snrs), "avg_launch_ms": avg_launch_s * 1e3},
-        "ber": {str(s): ber[s] for s in snrs},
-        "bler": {str(s): bler[s] for s in snrs},
-        "ber_match": ber_match,
-        "ber_db_offset": ber_db_offset,
-        "ber_reference": "tests/golden/sc_anchors_64_32.npz: the reference's sc_decode_new, 2e5 words at 0-1 dB, 1e6 "
-                         f"at 2-4 dB; this run: {B} distinct words per SNR",
-    }
-    if metric_as_named is not None:
-        out["metric_as_named"] = metric_as_named
-    out.update(legs)
     if not args.no_traffic and world == 1:
-        traffic, how = pmc_traffic(args)
-        out["roofline"]["traffic"] = None if traffic is None else traffic[KERNEL_NAME.split("<")[0]]
-        out["roofline"]["traffic_source"] = how
-        if "pac_sc" in out:
-            out["pac_sc"]["roofline"]["traffic"] = None if traffic is None else traffic[PAC_KERNEL]
-            out["pac_sc"]["roofline"]["traffic_source"] = how + "; the 2 dB launch of 2^20 words"
+        traffic, how, raw = pmc_traffic(args)
+        if traffic is not None:
+            headline["roofline"]["traffic"] = traffic[GRU_KERNEL]
+            headline["roofline"]["traffic_raw"] = raw[GRU_KERNEL]
+            headline["roofline"]["sc_launch"]["traffic"] = traffic[KERNEL_NAME.split("<")[0]]
+            sc1["roofline"]["traffic"] = traffic[KERNEL_NAME.split("<")[0]]
+            if "pac_sc" in legs:
+                legs["pac_sc"]["roofline"]["traffic"] = traffic[PAC_KERNEL]
+        headline["roofline"]["traffic_source"] = how + "; per launch, first (cold) launch skipped"
     if not args.no_cpu_baseline and world == 1:
+        net32, _, _, _ = crisp_model(code, dev)
+        yh = [y[:4096].cpu().numpy() for y in ys]
+        headline["cpu_baseline"] = cpu_baseline_sc_gru(yh, snrs, info, net32, args.cpu_seconds)
         ys_host = [y[: 1 << 18].cpu().numpy() for y in ys]
-        out["cpu_baseline"] = cpu_baseline(ys_host, snrs, code.info_positions, args.cpu_seconds)
-        if metric_as_named is not None:
-            net, _, _, _ = crisp_model(code, dev)
-            yh = [y[:4096].cpu().numpy() for y in ys]
-            out["metric_as_named"]["cpu_baseline"] = cpu_baseline_sc_gru(yh, snrs, code.info_positions, net,
-                                                                         args.cpu_seconds)
-    print(json.dumps(out), flush=True)
+        sc1["cpu_baseline"] = cpu_baseline(ys_host, snrs, info, args.cpu_seconds)
+    full.update(legs)
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(args.full_json)), exist_ok=True)
+        with open(args.full_json, "w") as f:
+            json.dump(full, f, indent=1)
+        headline["full_record"] = os.path.relpath(os.path.abspath(args.full_json), ROOT)
+    except OSError as e:
+        headline["full_record"] = f"not written: {e}"
+    headline.update(compact_configs(legs, gvr))
+    print(json.dumps(headline), flush=True)
     return 0
+
+
+def compact_configs(legs, gvr):
+    """One small summary per configuration for the printed line (the full records are in the --full-json file)."""
+    def r3(x):
+        return None if x is None else float(f"{x:.4g}")
+
+    out = {"gru_vs_reference_within_4_sigma": None if gvr is None else gvr["within_4_sigma"]}
+    c = {}
+    if "configs1_sc" in legs:
+        l1 = legs["configs1_sc"]
+        c["1_sc_decode"] = {"value": r3(l1["value"]), "hbm_frac": r3(l1["roofline"]["frac"]),
+                            "ber_match_0.05dB": l1.get("ber_match")}
+    if "fp32_path" in legs:
+        c["1+2_step_fp32_gru"] = {"value": r3(legs["fp32_path"]["value"]),
+                                  "fp32_mfma_frac": r3(legs["fp32_path"]["roofline"]["frac"])}
+    if "crisp_gru" in legs:
+        g = legs["crisp_gru"]
+        c["2_crisp_gru_alone"] = {"fp32": r3(g["value"]), "fp16x3_launch_ms": r3(g["fp16x3"]["avg_launch_ms"])}
+    if "pac_gru" in legs:
+        c["3_pac_gru"] = {"value": r3(legs["pac_gru"]["value"]), "fp32_mfma_frac": r3(legs["pac_gru"]["frac"])}
+    if "pac_sc" in legs:
+        c["3_pac_sc"] = {"value": r3(legs["pac_sc"]["value"]), "hbm_frac": r3(legs["pac_sc"]["roofline"]["frac"])}
+    if "conv_model" in legs:
+        cm = legs["conv_model"]
+        c["4_conv_model"] = {"value": r3(cm["value"]), "fp16_issued_frac": r3(cm["roofline"]["frac"]),
+                             "fp32_path": r3(cm["fp32_path"]["value"])}
+    if "montecarlo" in legs:
+        c["montecarlo_fused_sc"] = r3(legs["montecarlo"]["value"])
+    out["configs_summary"] = c
+    return out
 
 
 if __name__ == "__main__":

@@ -133,10 +133,16 @@ def rnn_from_checkpoint(ckpt, device="cuda", precision="fp32"):
     onehot = bool(getattr(a, "onehot", False))
     N = int(a.N)
     din = (N if dtype == "y_input" else 0) + 1 + int(onehot)
-    yh, yd = (0, 0) if dtype == "y_input" else (int(getattr(a, "y_hidden_size", 128)), int(getattr(a, "y_depth", 3)))
+    # the reference's constructors (rnn_all.py:1316-1320): y_h0 builds out_linear_depth 1 whatever the flag says;
+    # y_input (no --use_ynn) passes y_hidden_size only for an out_linear_depth > 1 head
+    old = int(getattr(a, "out_linear_depth", 1)) if dtype == "y_input" else 1
+    if dtype == "y_input":
+        yh, yd = (int(getattr(a, "y_hidden_size", 128)) if old > 1 else 0), 0
+    else:
+        yh, yd = int(getattr(a, "y_hidden_size", 128)), int(getattr(a, "y_depth", 3))
     net = RNN_Model(getattr(a, "rnn_type", "GRU"), din, int(a.rnn_feature_size), 1, int(a.rnn_depth), N,
                     yh, yd, getattr(a, "activation", "selu"), float(getattr(a, "dropout", 0.0)),
-                    bool(getattr(a, "use_skip", False)), out_linear_depth=int(getattr(a, "out_linear_depth", 1)),
+                    bool(getattr(a, "use_skip", False)), out_linear_depth=old,
                     bidirectional=bool(getattr(a, "bidirectional", False)),
                     use_layernorm=bool(getattr(a, "use_layernorm", False))).to(device)
     net.load_state_dict(ckpt["net"])

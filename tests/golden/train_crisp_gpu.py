@@ -142,6 +142,10 @@ def main():
     ap.add_argument("--miopen", action="store_true", help="nn.GRU through MIOpen (default: PyTorch's native GRU)")
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu")
     ap.add_argument("--threads", type=int, default=None)
+    ap.add_argument("--amp", choices=["none", "bf16"], default="none",
+                    help="bf16 autocast of the forward (training speed only; the fixture is whatever weights result, "
+                         "and every parity claim rests on the reference's fp32 decoder run on them)")
+    ap.add_argument("--probe", type=int, default=0, help="time this many steps and exit (no state written)")
     ap.add_argument("--init", default=None, help="weights ({'net': state_dict}) to start the first GPU stage from "
                                                   "(the reference-loop stages before the GPU block)")
     args = ap.parse_args()
@@ -195,14 +199,20 @@ def main():
             gt = torch.ones(c["batch"], N, device=dev)
             gt[:, info_t] = msg
             y = enc(msg) + sigma * torch.randn(c["batch"], N, device=dev)
-            decoded = teacher_forced(net, y, gt)
-            loss = loss_fn(decoded[:, info_t], msg)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp == "bf16"):
+                decoded = teacher_forced(net, y, gt)
+            loss = loss_fn(decoded[:, info_t].float(), msg)
             loss.backward()
             torch.nn.utils.clip_grad_norm_(net.parameters(), 0.25)
             opt.step()
             opt.zero_grad()
             sched.step()
             now = time.time()
+            if args.probe and step + 1 - s0 == args.probe:
+                torch.cuda.synchronize()
+                print(f"PROBE {args.case} amp={args.amp} miopen={args.miopen}: "
+                      f"{args.probe / (time.time() - t0):.2f} steps/s (incl. warm-up)", flush=True)
+                return
             if now - last_print > 30 or step == steps - 1:
                 rate = (step + 1 - s0) / max(now - t0, 1e-9)
                 print(f"[{args.case}] stage {si + 1}/{len(stages)} K={K} step {step + 1}/{steps} "

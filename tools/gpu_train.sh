@@ -10,5 +10,5 @@ for c in "$@"; do
   INIT=""
   [ -f train_state/$c.init.pt ] && INIT="--init train_state/$c.init.pt"
   timeout -k 10 $((B + 120)) python -u tests/golden/train_crisp_gpu.py $c --state gpurun_out/train/$c.pt \
-      --out gpurun_out/train/$c.net.pt --budget-s $B $INIT 2>&1 | tee -a gpurun_out/train/$c.log
+      --out gpurun_out/train/$c.net.pt --budget-s $B $INIT ${TRAIN_ARGS:-} 2>&1 | tee -a gpurun_out/train/$c.log
 done
