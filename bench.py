@@ -868,22 +868,19 @@ def main():
         "value": value, "unit": "codewords/s (each decoded by SC and by the CRISP GRU)",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp16x3 GRU (hi + lo fp16 operands on v_mfma_f32_16x16x32_f16, fp32 accumulation and gates); fp32 SC",
-        "data": "synthetic (Philox msg -> Plotkin encode -> AWGN), resident in HBM before timing; GRU weights "
-                + wdesc,
-        "config": {"workload": "configs[1]+[2]: Polar(N=64,K=32) eval step (rnn_all.py:853-880): min-sum SC sweep launch "
-                               "+ per SNR point a CRISP GRU decode (hidden 64, 2 layers, onehot y_input) + device "
-                               "BER/BLER counts of both, 2^20 words per SNR per GPU, SNR 0-4 dB",
+        "dtype": "fp16x3 GRU (hi+lo fp16 MFMA operands, fp32 accumulate/gates); fp32 SC",
+        "data": "synthetic Philox AWGN words, resident in HBM; GRU weights " + wdesc,
+        "config": {"workload": "configs[1]+[2]: Polar(64,32) eval step (rnn_all.py:853-880): SC sweep launch + per SNR "
+                               "a CRISP GRU decode (hidden 64, 2 layers) + BER/BLER counts, 2^20 words/SNR/GPU, 0-4 dB",
                    "code": "Polar(64,32) 'polar' rate profile", "batch_per_snr_per_gpu": B, "snr_db": snrs,
                    "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
         "world_size_rccl": world, "rank_ms_per_step": rank_ms,
         "roofline": {"bound": "mfma", "kernel": "gru16p_kernel<5> (fp16x3 CRISP GRU, one launch per SNR point)",
                      "achieved": tf16, "peak": FP16_PEAK_TF, "unit": "TFLOP/s", "frac": tf16 / FP16_PEAK_TF,
                      "traffic": None,
-                     "algorithmic": f"{flop_cw:.4g} FLOP per codeword (SURVEY.md 8(d): y.W_ih once + 64 steps of both "
-                                    f"layers' gate GEMVs + output dot) x {B} codewords per launch",
+                     "algorithmic": f"{flop_cw:.4g} FLOP/codeword (SURVEY.md 8(d)) x {B} codewords per launch",
                      "issued_frac": 3 * tf16 / FP16_PEAK_TF,
-                     "issued_note": "the split issues 3 fp16 products per multiply (hi.hi + hi.lo + lo.hi)",
+                     "issued_note": "3 fp16 products per multiply (hi.hi + hi.lo + lo.hi)",
                      "avg_launch_ms": gru_ms,
                      "sc_launch": {"bound": "hbm", "kernel": KERNEL_NAME, "achieved": sc_gbs, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": sc_gbs / HBM_PEAK_GBS, "avg_launch_ms": sc_ms,
@@ -936,7 +933,7 @@ def main():
             sc1["roofline"]["traffic"] = traffic[KERNEL_NAME.split("<")[0]]
             if "pac_sc" in legs:
                 legs["pac_sc"]["roofline"]["traffic"] = traffic[PAC_KERNEL]
-        headline["roofline"]["traffic_source"] = how + "; per launch, first (cold) launch skipped"
+        headline["roofline"]["traffic_source"] = how
     if not args.no_cpu_baseline and world == 1:
         net32, _, _, _ = crisp_model(code, dev)
         yh = [y[:4096].cpu().numpy() for y in ys]
@@ -952,8 +949,19 @@ def main():
     except OSError as e:
         headline["full_record"] = f"not written: {e}"
     headline.update(compact_configs(legs, gvr))
-    print(json.dumps(headline), flush=True)
+    print(json.dumps(_round_floats(headline)), flush=True)
     return 0
+
+
+def _round_floats(x, keep=("value", "ms_per_step")):
+    """5 significant digits for the printed line (the full record keeps full precision)."""
+    if isinstance(x, dict):
+        return {k: (v if k in keep else _round_floats(v, keep)) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_round_floats(v, keep) for v in x]
+    if isinstance(x, float):
+        return float(f"{x:.5g}")
+    return x
 
 
 def compact_configs(legs, gvr):

@@ -1108,20 +1108,13 @@ __device__ __forceinline__ f4 fma4(float x, const f4& c, const f4& p) {
 // element i, stage 0 exp2s / 1 rcps + n-gate input + exp2 / 2 rcp + blend), spread over its MFMA triples between
 // sched_barrier fences; the h1 update of tile 3, the output, the decision and the h1 split ride on the NEXT step's
 // layer-0 tile-0 GEMM (which needs only h0', not x_i: the x_i column and P are added after it).
-#ifndef NPD_GRU16_ORDER
-#define NPD_GRU16_ORDER 0
-#endif
-// chunk C -> (element, stage).  Order 0: element-major (consecutive chunks are stages of one element: dependent);
-// order 1: skewed wavefront, so the two chunks sharing an MFMA region belong to different elements
-__device__ constexpr int kOrdE[12] = {0, 1, 2, 0, 3, 1, 2, 0, 3, 1, 2, 3};
-__device__ constexpr int kOrdS[12] = {0, 0, 0, 1, 0, 1, 1, 2, 1, 2, 2, 2};
 template <int SPLIT>
 struct Upd4 {
     f4 er, ez, en, z;
     template <int C>
     __device__ __forceinline__ void step(f4& h, const f4& ar, const f4& az, const f4& ain, const f4& ahn) {
         constexpr float c1 = SplitT<SPLIT>::kC1, c2 = SplitT<SPLIT>::kC2;
-        constexpr int i = NPD_GRU16_ORDER == 1 ? kOrdE[C] : C / 3, st = NPD_GRU16_ORDER == 1 ? kOrdS[C] : C % 3;
+        constexpr int i = C / 3, st = C % 3;
         if constexpr (st == 0) {
             er[i] = __builtin_amdgcn_exp2f(c1 * ar[i]);
             ez[i] = __builtin_amdgcn_exp2f(c1 * az[i]);

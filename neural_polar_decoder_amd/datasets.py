@@ -122,27 +122,29 @@ def code_from_args(args):
 
 def rnn_from_checkpoint(ckpt, device="cuda", precision="fp32"):
     """(net, RNN_decoder, code) of a CRISP checkpoint ({'net', 'args'}, rnn_all.py:1310-1330): decoding_type y_input
-    without the y-MLP (the CRISP scripts) or y_h0 with it (rnn_all.py:1316-1317), GRU or LSTM cells."""
+    without the y-MLP (the CRISP scripts) or with --use_ynn's (rnn_all.py:1319), or y_h0 with its y-MLP
+    (rnn_all.py:1316-1317), GRU or LSTM cells."""
     from .rnn import RNN_Model, RNN_decoder
     if isinstance(ckpt, str):
         ckpt = load_checkpoint(ckpt)
     a = ckpt["args"]
     dtype = getattr(a, "decoding_type", "y_input")
-    if dtype not in ("y_input", "y_h0") or (dtype == "y_input" and getattr(a, "use_ynn", False)):
-        raise NotImplementedError("fused decode supports decoding_type 'y_input' without --use_ynn, and 'y_h0'")
+    if dtype not in ("y_input", "y_h0"):
+        raise NotImplementedError("fused decode supports decoding_type 'y_input' (with or without --use_ynn) and 'y_h0'")
+    ynn = dtype == "y_input" and bool(getattr(a, "use_ynn", False))
     onehot = bool(getattr(a, "onehot", False))
     N = int(a.N)
     din = (N if dtype == "y_input" else 0) + 1 + int(onehot)
     # the reference's constructors (rnn_all.py:1316-1320): y_h0 builds out_linear_depth 1 whatever the flag says;
     # y_input (no --use_ynn) passes y_hidden_size only for an out_linear_depth > 1 head
     old = int(getattr(a, "out_linear_depth", 1)) if dtype == "y_input" else 1
-    if dtype == "y_input":
+    if dtype == "y_input" and not ynn:
         yh, yd = (int(getattr(a, "y_hidden_size", 128)) if old > 1 else 0), 0
-    else:
+    else:  # y_h0, or y_input --use_ynn (rnn_all.py:1319: the y-MLP with y_output_size = N)
         yh, yd = int(getattr(a, "y_hidden_size", 128)), int(getattr(a, "y_depth", 3))
     net = RNN_Model(getattr(a, "rnn_type", "GRU"), din, int(a.rnn_feature_size), 1, int(a.rnn_depth), N,
                     yh, yd, getattr(a, "activation", "selu"), float(getattr(a, "dropout", 0.0)),
-                    bool(getattr(a, "use_skip", False)), out_linear_depth=old,
+                    bool(getattr(a, "use_skip", False)), out_linear_depth=old, y_output_size=N if ynn else None,
                     bidirectional=bool(getattr(a, "bidirectional", False)),
                     use_layernorm=bool(getattr(a, "use_layernorm", False))).to(device)
     net.load_state_dict(ckpt["net"])

@@ -19,9 +19,10 @@ from . import _lib
 
 class RNN_Model(nn.Module):
     """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts nets with output_size 1,
-    out_linear_depth 1, unidirectional, no layernorm: GRU with decoding_type 'y_input' and y_depth 0 (the CRISP
-    scripts, rnn_all.py:250-253) or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip);
-    LSTM (rnn_all.py:69) with 'y_input', fp32, hidden 32 or hidden 64 with one layer."""
+    out_linear_depth 1, unidirectional, no layernorm: GRU with decoding_type 'y_input' -- y_depth 0 (the CRISP
+    scripts, rnn_all.py:250-253) or --use_ynn's y-MLP of N outputs feeding the GRU in place of y (rnn_all.py:1319-1320,
+    :533-536) -- or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip); LSTM
+    (rnn_all.py:69) with 'y_input', fp32, hidden 32 or hidden 64 with one layer."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -80,6 +81,18 @@ class RNN_Model(nn.Module):
         x = x.contiguous()
         return x if self.rnn_type == "GRU" else (x, x)
 
+    def get_Fy(self, y):
+        """rnn_all.py:377-383 in PyTorch (--use_ynn): the y-MLP with get_h0's activation rule, no reshape.  The fused
+        decoder runs it on npd_ymlp_layer."""
+        x = y.clone()
+        for ii, layer in enumerate(self.y_linears):
+            x = layer(x) if ii == self.y_depth else self.act(layer(x))
+        return x
+
+    def _ymlp_ok(self, out_size):
+        return (hasattr(self, "y_linears") and not self.skip and self.activation in self.ACTS
+                and self.y_output_size == out_size)
+
     def forward(self, input, hidden, Fy=None):
         """Single recurrent step (rnn_all.py:387-398) -- the training-time API."""
         out, hidden = self.rnn(input, hidden)
@@ -95,9 +108,9 @@ class RNN_Model(nn.Module):
                     and (self.feature_size == 32 or (self.feature_size == 64 and self.num_rnn_layers == 1)))
         base = common and self.rnn_type == "GRU" and self.feature_size in (32, 64, 128, 256, 512)
         if decoding_type == "y_h0":
-            return (base and hasattr(self, "y_linears") and not self.skip and self.activation in self.ACTS
-                    and self.y_output_size == self.num_rnn_layers * self.feature_size)
-        return base and self.y_depth == 0
+            return base and self._ymlp_ok(self.num_rnn_layers * self.feature_size)
+        # y_input: y itself (y_depth 0) or --use_ynn's Fy = get_Fy(y) with N outputs (rnn_all.py:533-536)
+        return base and (self.y_depth == 0 or self._ymlp_ok(self.y_size))
 
 
 def pack_gru_weights(net: nn.Module, layers: int, y_cols: int = 0) -> np.ndarray:
@@ -185,6 +198,8 @@ class RNN_decoder:
             raise ValueError(f"net.input_size must be {'N + ' if self.decoding_type == 'y_input' else ''}1 + onehot")
         y_in = y
         y = _lib.f32c(_lib.stage(y, "y"))
+        if self.decoding_type == "y_input" and net.y_depth > 0:
+            y = _ymlp_forward(net, y)  # --use_ynn: Fy = net.get_Fy(y) replaces y as the GRU input (rnn_all.py:533-536)
         B = y.shape[0]
         if loss_inds is None:
             loss_inds = self.info_inds
@@ -208,9 +223,9 @@ class RNN_decoder:
 
 
 def _ymlp_forward(net: RNN_Model, y: torch.Tensor) -> torch.Tensor:
-    """get_h0's MLP (rnn_all.py:362-375) on npd_ymlp_layer: (B, N) -> (B, F * layers), layer ii followed by the
-    activation iff ii != y_depth (RNN_Model.get_h0).  Returns x before the reshape: element f * layers + l = layer l's
-    initial state of unit f."""
+    """The y-MLP (rnn_all.py:362-383: get_h0 / get_Fy) on npd_ymlp_layer: (B, N) -> (B, y_output_size), layer ii followed
+    by the activation iff ii != y_depth.  y_h0: x before get_h0's reshape (element f * layers + l = layer l's initial
+    state of unit f); --use_ynn: Fy."""
     L = _lib.load()
     x = y
     step = 65535 * 64

@@ -37,18 +37,18 @@ CASES = {
     "trained_crisp_64_32_h2e": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6432,
                                     curriculum=_cur(8, 5000, 32, 2000, 30000, 1000), ref_lr=2e-4,
                                     n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
-    # PAC(128,64) (configs[3], rnn_all.py:61 --code PAC, rate profile 'RM' reversed = hard first) at the CRISP script's
-    # own width (run_crisp.sh: --rnn_feature_size 512): K = 8 .. 64 on the GPU, then the reference's loop.  At hidden 64
-    # the same curriculum stalled (per-bit BER 0.08-0.26 even at 10 dB by K = 12, in either bit order).  NOT GENERATED:
-    # this F = 512 run learned through K = 28 (BLER 0.71 / 0.38 / 0.12 at 0 / 2 / 4 dB) and collapsed to coin flips by
-    # K = 61 (BER 0.45-0.49) with 400-step stages (the reference runs 5000); DESIGN.md 2b
     # run_crisp.sh's own decoder: Polar(64,22), rate profile rev_polar (hard first), GRU hidden 512, 2 layers, onehot
     # y_input, K = 8 .. 22 with K + 1 per stage.  The script runs 10000 steps at K = 8, 5000 per later stage and 100000 at
     # K = 22 (175k steps); this case runs the same stage order on the GPU with shortened stages (a GPU-minute budget),
     # then the reference's rnn_all.py for the last stage.
     "trained_crisp_64_22_f512": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=22, F=512, seed_init=6422,
                                      curriculum=_cur(8, 6000, 22, 1500, 20000, 20), ref_lr=2e-4,
-                                     n_logit=128, n_sc=1 << 14, n_dec=2048, n_mc=1 << 16, seed_dec=59, seed_mc=61),
+                                     n_logit=128, n_sc=1 << 14, n_dec=2048, n_mc=1 << 17, seed_dec=59, seed_mc=61),
+    # PAC(128,64) (configs[3], rnn_all.py:61 --code PAC, rate profile 'RM' reversed = hard first) at the CRISP script's
+    # own width (run_crisp.sh: --rnn_feature_size 512): K = 8 .. 64 on the GPU, then the reference's loop.  At hidden 64
+    # the same curriculum stalled (per-bit BER 0.08-0.26 even at 10 dB by K = 12, in either bit order).  NOT GENERATED:
+    # this F = 512 run learned through K = 28 (BLER 0.71 / 0.38 / 0.12 at 0 / 2 / 4 dB) and collapsed to coin flips by
+    # K = 61 (BER 0.45-0.49) with 400-step stages (the reference runs 5000); DESIGN.md 2b
     "trained_pac_128_64_f512": dict(_COMMON, code="PAC", profile="rev_RM", N=128, K=64, F=512, seed_init=12866,
                                     curriculum=_cur(8, 2000, 64, 400, 10000, 20), ref_lr=2e-4,
                                     n_logit=64, n_sc=1 << 13, n_dec=4096, n_mc=1 << 16, seed_dec=47, seed_mc=53),

@@ -478,6 +478,42 @@ def gen_gru_yh0():
              **{"w." + k: v for k, v in sd.items()})
 
 
+def gen_gru_ynn():
+    """decoding_type 'y_input' with --use_ynn (rnn_all.py:1319-1320: y_output_size = N, the y-MLP's output replaces y as
+    the GRU input; decode test branch rnn_all.py:533-536 Fy = net.get_Fy(y), then the y_input loop on [Fy, onehot]):
+    seeded PyTorch-default weights, Polar codes, reference encoder / channel at 0-4 dB, logits by a hook on net.linear."""
+    cases = [("gru_ynn_polar_64_32", 64, 32, 64, 2, True, False, "selu", 128, 3, 512, 5001),
+             ("gru_ynn_polar_32_16_f32_tanh_rev", 32, 16, 32, 1, True, True, "tanh", 64, 2, 256, 5002),
+             ("gru_ynn_polar_16_8_d1_noonehot", 16, 8, 64, 2, False, False, "relu", 32, 1, 256, 5003)]
+    for name, N, K, F, L, onehot, rev, act, yh, yd, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        net = rnn_m.RNN_Model("GRU", N + 1 + int(onehot), F, 1, L, N, yh, yd, act, 0.0, False, y_output_size=N,
+                              out_linear_depth=1)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_input", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits, fys = [], [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+                fy = net.get_Fy(y)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+            fys.append(fy.numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), fy=np.concatenate(fys), info=info, N=N, K=K, F=F, layers=L,
+             onehot=int(onehot), rev=int(rev), activation=np.bytes_(act), y_hidden=yh, y_depth=yd,
+             **{"w." + k: v for k, v in sd.items()})
+
+
 def gen_lstm():
     """--rnn_type LSTM (rnn_all.py:69) with decoding_type y_input (rnn_all.py:532-547: hidden = (h, c) zeros): seeded
     PyTorch-default weights, Polar codes, reference encoder / channel at 0-4 dB, logits by a hook on net.linear."""
@@ -554,6 +590,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "lstm", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_ynn", "lstm", "conv"]
     for w in which:
         globals()["gen_" + w]()

@@ -142,12 +142,13 @@ def test_conv_fp16x3_error_matches_fp32_against_float64(oracle):
 def test_conv_fp16x3_shapes_vs_oracle(oracle, E, N):
     """The fp16x3 kernels at every shape family they dispatch on, against the float64 oracle on a ragged batch of more
     than one 4096-codeword chunk (seeded weights, conftest.conv_weights_from_seed): embed 64 / N 128 (weight-stationary
-    conv kernel with 32-channel groups, 128-position items; the 128 x 128 FC kernel for all three Linear layers); embed
-    64 / N 64 (the 64-channel layer on 64-position items);
+    conv kernel (conv_ws2_kernel) with 32-channel groups, 128-position items; the 128 x 128 FC kernel for all three Linear
+    layers); embed 64 / N 64 (the 64-channel layer on 64-position items);
     embed 80 / N 64 (40-channel layers = three 16-channel groups, 64-position items; the 80-channel layer on the
     slab kernel; FC1 / FC2 of 64 outputs on the 64 x 64 FC kernel); embed 96 / N 64 (48-channel layers, the 96-channel
-    layer on the slab kernel); C5 (embed 128, N 256: 64-channel layers on 8 waves in 2 channel parts, the 128-channel
-    layer in 4). Same bars as the golden tests: logits within 1e-5, decisions identical away from zero."""
+    layer on the slab kernel); C5 (embed 128, N 256: 64-channel layers on 8 waves in 4 channel parts, the 128-channel
+    layer on 32 output channels in 8 parts). Same bars as the golden tests: logits within 1e-5, decisions identical away
+    from zero."""
     sd = conv_weights_from_seed(E, N, 100 + E)
     net = net_from(sd, E, N, precision="fp16x3")
     rng = np.random.default_rng(E + N)
@@ -157,3 +158,25 @@ def test_conv_fp16x3_shapes_vs_oracle(oracle, E, N):
     sel = np.r_[0:B:97, B - 1]
     ref = oracle.conv_forward(y[sel], sd)
     check(lg.cpu().numpy()[sel], dec.cpu().numpy()[sel], ref)
+
+
+@pytest.mark.parametrize("E,N", [(64, 128), (128, 256), (80, 64)])
+def test_conv_fp16x3_large_activations(oracle, E, N):
+    """Activations far beyond fp16's range (received words x 3e4: conv and Linear inputs up to ~1e5): the split kernels
+    scale each layer's input by 2^SA with SA from the producing kernel's max |a| (npd_conv.hip split_sa), so hi never
+    overflows -- before that fix the fixed 2^4 scale turned every |a| > 4094 into inf and the logits into NaN.  The
+    logits stay finite and match the float64 oracle (LayerNorm brings them back to O(1); 1e-4 absolute, the fp32 rounding of
+    pre-LayerNorm values ~1e5 x 2^-24 relative to their spread) and the fp32 path's decisions."""
+    sd = conv_weights_from_seed(E, N, 100 + E)
+    rng = np.random.default_rng(5 + E)
+    B = 257
+    y = (3e4 * (np.where(rng.random((B, N)) < 0.5, -1.0, 1.0) + 0.8 * rng.standard_normal((B, N)))).astype(np.float32)
+    lg16, dec16 = net_from(sd, E, N, precision="fp16x3").logits(torch.from_numpy(y).to(DEV))
+    lg32, _ = net_from(sd, E, N, precision="fp32").logits(torch.from_numpy(y).to(DEV))
+    lg16, lg32 = lg16.cpu().numpy(), lg32.cpu().numpy()
+    assert np.isfinite(lg16).all()
+    ref = oracle.conv_forward(y[::8], sd)
+    assert np.abs(lg16[::8] - ref).max() < 1e-4, float(np.abs(lg16[::8] - ref).max())
+    assert np.abs(lg16 - lg32).max() < 1e-4
+    sure = np.abs(ref) > 1e-4
+    assert np.array_equal(dec16.cpu().numpy()[::8][sure], np.sign(ref)[sure])

@@ -7,7 +7,8 @@ words per SNR through convNet.decode on the CPU).
 
 Tolerance (as tests/test_conv_gpu.py for logits, as tests/test_trained_gru_gpu.py for the curve):
   (a) decisions on the fixture words: >= 99.9 % of information bits and >= 99 % of codewords identical to the
-      reference's; logits within 1e-5 absolute;
+      reference's; logits within 1e-4 absolute (ATOL: the trained net's reference fp32 logits themselves sit up to
+      3.1e-5 from float64, so the seeded nets' 1e-5 bar of tests/test_conv_gpu.py does not apply);
   (b) Monte-Carlo at 2^18 Philox words per SNR: BLER and BER within 4 two-sample standard errors of the reference's
       curve, and the BLER curve's horizontal offset within +-0.05 dB at every point whose reference BLER is in
       [1e-3, 0.9].

@@ -31,7 +31,7 @@ def child():
         dec = RNN_decoder("y_input", 64, code.info_positions, onehot=True, precision=prec)
         dd, lg = dec.decode(net, False, y, return_logits=True)
         res[prec] = (dd, lg)
-        if prec == "fp16x3":
+        if True:
             for _ in range(2):
                 dec.decode(net, False, y)
             torch.cuda.synchronize()
@@ -41,7 +41,7 @@ def child():
                 dec.decode(net, False, y)
             e.record()
             torch.cuda.synchronize()
-            out["ms"] = s.elapsed_time(e) / 5
+            out["ms" if prec == "fp16x3" else "ms_fp32"] = s.elapsed_time(e) / 5
     same = (res["fp32"][0] == res["fp16x3"][0]).all(1)
     out["cw_agree"] = same.float().mean().item()
     out["max_logit_diff"] = (res["fp32"][1][same] - res["fp16x3"][1][same]).abs().max().item()
@@ -66,7 +66,7 @@ def main():
                 return 1
             res = json.loads(line[7:])
             print(f"round {r} {os.path.basename(lib):28s} {res['ms']:8.3f} ms/2^20  cw_agree {res['cw_agree']:.6f}  "
-                  f"max_logit_diff {res['max_logit_diff']:.2e}", flush=True)
+                  f"max_logit_diff {res['max_logit_diff']:.2e}  fp32 kernel {res['ms_fp32']:.2f} ms", flush=True)
     return 0
 
 
