@@ -402,27 +402,52 @@ def gru_leg(code, dev, y, B, world, timer):
             "config": "configs[2]: Polar(64,32) CRISP GRU hidden 64, 2 layers, onehot y_input, 2 dB, 2^20 per GPU"}
 
 
+TRAINED_F512 = os.path.join(ROOT, "tests", "golden", "trained_crisp_64_22_f512.npz")
+
+
 def crisp_f512_leg(dev, rank, world, timer, B=1 << 15):
-    """The CRISP curriculum's decoder (run_crisp.sh): Polar(64,22) rev_polar profile, GRU hidden 512,
-    2 layers, onehot; fp32 weight-streaming MFMA kernel (weights 9.4 MB, read from L2/MALL each step)."""
+    """The CRISP curriculum's decoder (run_crisp.sh): Polar(64,22) rev_polar profile, GRU hidden 512, 2 layers, onehot;
+    fp32 weight-streaming MFMA kernel (weights 9.4 MB, read from L2/MALL each step).  Weights: the trained fixture
+    (tests/golden/crisp_cases.py trained_crisp_64_22_f512: run_crisp.sh's stage order on the GPU, last stage by the
+    reference's rnn_all.py) when present, with its BER/BLER at 0-4 dB against the reference's own curve for the same
+    weights; else seeded."""
     import argparse as _ap
     from neural_polar_decoder_amd import PolarCode
     from neural_polar_decoder_amd.codes import polar_info_positions
-    from neural_polar_decoder_amd.montecarlo import seeded_crisp
     info = polar_info_positions(64, 22, "rev_polar", 22)
     code = PolarCode(6, 22, _ap.Namespace(), F=np.setdiff1d(np.arange(64), info))
-    net, dec = seeded_crisp(code, 512, 2, seed=0, device=dev)
+    fix = None
+    if os.path.exists(TRAINED_F512):
+        net, dec, wdesc, fix = trained_or_seeded(code, TRAINED_F512, code.info_positions, dev)
+    else:
+        from neural_polar_decoder_amd.montecarlo import seeded_crisp
+        net, dec = seeded_crisp(code, 512, 2, seed=0, device=dev)
+        wdesc = "seeded untrained weights"
     _, _, y = code.mc_generate(B, 0.0, SEED, 0, rank * B, device=dev, want_msg=False)
     stream = torch.cuda.current_stream(dev)
     t = timer(lambda: dec.decode(net, False, y), iters=1, warm=1)
     ms = event_ms(lambda: dec.decode(net, False, y), 1, stream)
     flop_cw = gru_flop_per_cw(64, 512)
     tf = flop_cw * B / (ms / 1e3) / 1e12
-    return {"value": world * B / t, "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": ms,
-            "algorithmic_flop_per_cw": flop_cw, "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
-            "frac": tf / FP32_PEAK_TF, "dtype": "fp32 (v_mfma_f32_32x32x2_f32)",
-            "config": "run_crisp.sh decoder: Polar(64,22) rev_polar, CRISP GRU hidden 512, 2 layers, onehot, 0 dB, "
-                      "seeded untrained weights"}
+    out = {"value": world * B / t, "unit": "codewords/s", "batch_per_gpu": B, "avg_launch_ms": ms,
+           "algorithmic_flop_per_cw": flop_cw, "achieved_tflops": tf, "peak_tflops_fp32": FP32_PEAK_TF,
+           "frac": tf / FP32_PEAK_TF, "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "weights": wdesc,
+           "config": "run_crisp.sh decoder: Polar(64,22) rev_polar, CRISP GRU hidden 512, 2 layers, onehot, 0 dB"}
+    if fix is not None:  # the BER curve of the trained decoder against the reference's (2^17 words per SNR there)
+        from neural_polar_decoder_amd.utils import count_errors
+        snrs = [float(x) for x in fix["snr"]]
+        n = 1 << 17
+        c = torch.zeros(len(snrs), 2, dtype=torch.int64, device=dev)
+        for si, s_ in enumerate(snrs):
+            msg, _, ys = code.mc_generate(n, s_, SEED, si, rank * n, device=dev)
+            count_errors(msg, dec.decode(net, False, ys), c[si], cols=code.info_positions)
+        allreduce(c, _sum(), world)
+        cc = c.cpu().numpy()
+        out["gru_vs_reference"] = gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], world * n, 22)
+        ref_bler = [int(x) / int(fix["mc_n"]) for x in fix["mc_blk_err"]]
+        bl = [float(cc[i, 1]) / (world * n) for i in range(len(snrs))]
+        out["bler_db_offset_vs_reference"] = {str(s_): o for s_, o in zip(snrs, db_offsets(snrs, bl, snrs, ref_bler))}
+    return out
 
 
 def pac_legs(snrs, B, rank, world, timer, dev, do_gru, do_sc):
@@ -991,6 +1016,10 @@ def compact_configs(legs, gvr):
                              "fp32_path": r3(cm["fp32_path"]["value"])}
     if "montecarlo" in legs:
         c["montecarlo_fused_sc"] = r3(legs["montecarlo"]["value"])
+    if "crisp_gru_f512" in legs:
+        f = legs["crisp_gru_f512"]
+        c["crisp_f512"] = {"value": r3(f["value"]), "fp32_mfma_frac": r3(f["frac"]),
+                           "within_4_sigma": (f.get("gru_vs_reference") or {}).get("within_4_sigma")}
     out["configs_summary"] = c
     return out
 

@@ -50,6 +50,7 @@ struct LayerDesc {
 // so that max |w| 2^SW is in [2^12, 2^13) (hi and lo normal for |w| >= max |w| 2^-11)
 constexpr int kSplitSA = 4;
 
+
 // nn.GELU() (exact, erf form: x Phi(x)) without a branch: Phi(x) = 1 - q for x >= 0 and q for x < 0, where
 // q = erfc(|x| / sqrt 2) / 2 from the Chebyshev fit of erfc (Numerical Recipes, "erfcc": t exp(-z^2 + P(t)),
 // t = 1 / (1 + z / 2), fractional error < 1.2e-7 for all z >= 0) with log2 e and the 1/2 folded into P's coefficients.
@@ -75,21 +76,19 @@ __device__ __forceinline__ float gelu(float x) {
     return x * (x >= 0.0f ? 1.0f - q : q);
 }
 
-template <int N>
-struct IC {
-    static constexpr int value = N;
-};
-template <int B, int E, typename Fn>
-__device__ __forceinline__ void static_for(Fn&& f) {
-    if constexpr (B < E) {
-        f(IC<B>{});
-        static_for<B + 1, E>(f);
-    }
-}
+// The max |a| of one activation is kept in kAmaxSpread words kAmaxStride words apart (4 KB): each producing wave
+// atomicMax-es one of them (by block and wave), so tens of thousands of small blocks (layer 0) do not serialise on one
+// address; a consumer reads all of them with one load per lane and reduces over the wave.
+constexpr int kAmaxSpread = 64;
+constexpr int kAmaxStride = 16;
+constexpr int kAmaxWords = kAmaxSpread * kAmaxStride;  // per activation
 
 __device__ __forceinline__ int split_sa(const uint32_t* amax) {
     if (amax == nullptr) return kSplitSA;
-    const int e = (int)((__builtin_nontemporal_load(amax) >> 23) & 0xFFu) - 126;  // max |a| < 2^e
+    uint32_t m = __builtin_nontemporal_load(amax + (threadIdx.x & 63) * kAmaxStride);
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, k));
+    const int e = (int)((m >> 23) & 0xFFu) - 126;  // max |a| < 2^e
     return min(kSplitSA, 15 - e);
 }
 
@@ -101,7 +100,10 @@ __device__ __forceinline__ float amax4(const f4& v) {
 __device__ __forceinline__ void publish_amax(uint32_t* amax, float m) {
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) m = fmaxf(m, __shfl_xor(m, k));
-    if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        atomicMax(amax + ((blk * 8 + (threadIdx.x >> 6)) % kAmaxSpread) * kAmaxStride, __float_as_uint(m));
+    }
 }
 
 __device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
@@ -318,42 +320,44 @@ __global__ __launch_bounds__(256) void conv_layer_split_kernel(const float* __re
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
 
-// ------------------------------------------------------------------------------ conv layer, fp16x3, pipelined
-// conv_split_ws_kernel's products and arithmetic, software-pipelined so that each wave's vector work runs in the issue
-// gaps of its own MFMAs (a wave's VALU overlaps only its own MFMAs, profiles/round3/coissue.txt): while item i's MFMA
-// triples run, the same wave splits and stages item i+1's slab (fetched into registers during item i-1), issues the
-// global loads of item i+2's slab, and finishes item i-1 -- the partner parts' partial sums from LDS, descale, bias,
-// GELU, residual, store -- in chunks placed between the triples (sched_barrier fences).  After the MFMAs a wave writes
-// the partial sums it hands over to an LDS slot and loads the residual of the quads it finishes.  NSLOT = 2: two
-// slots, alternating, one barrier per item; NSLOT = 1 (where two do not fit in the LDS): a second barrier before the
-// slot is rewritten.  Channel parts: quad u (4 channels x 32 positions, 4 TPW per wave) is finished by part u % KS,
-// which sums the parts in order 0..KS-1 (deterministic).
-// Activation scale (fp16 range): the slab is split as fp16(a 2^SA) + fp16(a 2^SA - hi) with SA = min(4, 15 - E)
-// for max |a| < 2^E read from amax_in (the producing kernel's atomicMax of |a|), so hi never overflows whatever the
-// activations' range (SA = 4, as before, while max |a| < 2^11); the epilogue multiplies by 2^-(SW + SA) (exact) and
-// publishes max |output| to amax_out for the next layer.
-template <int NG, int Q, int KS, int NW, int NSLOT, int CO = 2>
-__global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_ws2_kernel(
-    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ res, const f4* __restrict__ wimg,
-    const float* __restrict__ bias, int cin, int cout, int N, int dil, int do_res, int sw,
-    const uint32_t* __restrict__ amax_in, uint32_t* __restrict__ amax_out, int64_t nb, int nslices) {
+// ------------------------------------------------------------------------------ conv layer, fp16x3, weight-stationary
+// The same products as conv_layer_split_kernel, reorganised so that nothing but activations streams: a persistent
+// block (one per CU) keeps its waves' weight slices in registers for the whole layer and walks (codeword, 64 Q-position
+// chunk) items.  NW waves = 2 (32 output channels each) x KS channel parts x NW / 2 / KS position parts; a wave holds
+// 32 channels x 7 taps x NG / KS 16-channel groups, hi and lo (56 NG / KS VGPRs).  NW = 8 (cin 64 / 96 / 128, KS 2 or
+// 4) keeps every wave under 256 registers, so two waves share each SIMD and one's MFMAs cover the other's LDS reads;
+// the KS channel parts of a tile hand each other their partial sums through LDS and the tile's finishing wave adds
+// them.  NW = 4, KS = 1 for cin <= 48.  The next item's slab (positions plus the dilation halo, all channels, fp32) is
+// fetched into registers before the current item's MFMAs and split into the other half of a double-buffered fp16
+// hi / lo LDS slab after them, so HBM reads overlap the matrix work and no weight fragment is re-read.  Dilation <= 4
+// (conv_spec) bounds the halo at 12.
+template <int NG, int Q, int KS, int NW>
+__global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_split_ws_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                const float* __restrict__ res,
+                                                                const f4* __restrict__ wimg,
+                                                                const float* __restrict__ bias, int cin, int cout,
+                                                                int N, int dil, int do_res, int sw,
+                                                                const uint32_t* __restrict__ amax_in,
+                                                                uint32_t* __restrict__ amax_out, int64_t nb, int nslices) {
     extern __shared__ __attribute__((aligned(16))) _Float16 slab16[];
+    const int sa = split_sa(amax_in);
+    const float sa_scale = __builtin_ldexpf(1.0f, sa), descale = __builtin_ldexpf(1.0f, -(sw + sa));
+    float amx = 0.0f;
     constexpr int NT = 64 * NW;
-    constexpr int PT = 64 * Q;        // positions per item
+    constexpr int PT = 64 * Q;        // positions per item (2 Q tiles of 32)
     constexpr int C4P = 4 * NG;       // float4 channel groups per staged row (pad channels zero)
     constexpr int CSH = 16 * NG + 8;  // fp16 row stride of the LDS slab
     constexpr int MAXE = ((PT + 24) * C4P + NT - 1) / NT;
-    constexpr int NGW = NG / KS;      // 16-channel groups per wave
-    constexpr int PS = NW / CO / KS;  // position parts
+    constexpr int NGW = NG / KS;      // channel groups per wave
+    constexpr int PS = NW / 2 / KS;   // position parts
     constexpr int TPW = 2 * Q / PS;   // 32-position tiles per wave
-    constexpr int NQ = 4 * TPW;       // quads per wave
-    constexpr int FQ = NQ / KS;       // quads this wave finishes
-    constexpr int NTR = 7 * NGW * TPW;  // MFMA triples per item
-    static_assert(NG % KS == 0 && (NW / CO) % KS == 0 && (2 * Q) % PS == 0 && NQ % KS == 0, "wave decomposition");
+    static_assert(NG % KS == 0 && (NW / 2) % KS == 0 && (2 * Q) % PS == 0, "wave decomposition");
+    // partial-sum slots per wave: KS = 2 with 2 tiles hands over exactly one (slot 0), else slot = tile
+    constexpr int RS = (KS == 2 && TPW == 2) ? 1 : TPW;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
-    const int co_sub = wave % CO, rest = wave / CO;
+    const int co_sub = wave & 1, rest = wave >> 1;
     const int kp = rest % KS, pp = rest / KS;
     const int g0 = kp * NGW;
     const int halo = 3 * dil;
@@ -361,10 +365,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_ws
     const int plane = W * CSH;
     const int c4n = cin >> 2;
     const int slice = blockIdx.x % nslices;
-    const int co_t32 = slice * CO + co_sub;
-    const int sa = split_sa(amax_in);
-    const float sa_scale = __builtin_ldexpf(1.0f, sa);
-    const float descale = __builtin_ldexpf(1.0f, -(sw + sa));
+    const int co_t32 = slice * 2 + co_sub;
     hf8 ah[7][NGW], al[7][NGW];
     {
         const f4* wq = wimg + (int64_t)co_t32 * 7 * NG * 128 + lane;
@@ -376,193 +377,128 @@ __global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_ws
                 al[t][g] = __builtin_bit_cast(hf8, wq[(t * NG + g0 + g) * 128 + 64]);
             }
     }
-    // partial-sum slots: [slot][co_sub][pp][quad u][writer part, KS - 1 of them: (part - u % KS - 1) mod KS][lane] f4
-    f4* const red = reinterpret_cast<f4*>(slab16 + (size_t)4 * plane);
-    constexpr int SLOT = CO * PS * NQ * (KS > 1 ? KS - 1 : 1) * 64;
-    auto red_at = [&](int slot, int u, int part) -> f4* {
-        const int w = (part - (u % KS) - 1 + KS) % KS;
-        return red + slot * SLOT + (((co_sub * PS + pp) * NQ + u) * (KS - 1) + w) * 64 + lane;
-    };
+    // KS > 1: partial sums of the channel parts, [wave][tile][register][lane]
+    float* const red = reinterpret_cast<float*>(slab16 + (size_t)4 * plane);
     const int chunks = N / PT;
     const int64_t items = nb * chunks;
     const int64_t stride = gridDim.x / nslices;
     int64_t item = blockIdx.x / nslices;
     f4 pre[MAXE];
-    auto fetch_e = [&](int64_t it, int e) {
+    auto fetch = [&](int64_t it) {
         const int64_t b = it / chunks;
         const int l0 = (int)(it - b * chunks) * PT;
         const f4* inb = reinterpret_cast<const f4*>(in + b * (int64_t)N * cin);
-        const int idx = tid + NT * e;
-        const int p = idx / C4P, c4 = idx - p * C4P;
-        const int l = l0 - halo + p;
-        f4 v = f4{0.f, 0.f, 0.f, 0.f};
-        if (p < W && c4 < c4n && l >= 0 && l < N) v = inb[(int64_t)l * c4n + c4];
-        pre[e] = v;
+#pragma unroll
+        for (int e = 0; e < MAXE; ++e) {
+            const int idx = tid + NT * e;
+            const int p = idx / C4P, c4 = idx - p * C4P;
+            const int l = l0 - halo + p;
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (p < W && c4 < c4n && l >= 0 && l < N) v = inb[(int64_t)l * c4n + c4];
+            pre[e] = v;
+        }
     };
-    auto stash_e = [&](int buf, int e) {
+    auto stash = [&](int buf) {
         _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
-        const int idx = tid + NT * e;
-        const int p = idx / C4P, c4 = idx - p * C4P;
-        if (p < W) {
-            hf4 hi, lo;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float x = pre[e][j] * sa_scale;
-                hi[j] = (_Float16)x;
-                lo[j] = (_Float16)(x - (float)hi[j]);
+        for (int e = 0; e < MAXE; ++e) {
+            const int idx = tid + NT * e;
+            const int p = idx / C4P, c4 = idx - p * C4P;
+            if (p < W) {
+                hf4 hi, lo;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float x = pre[e][j] * sa_scale;
+                    hi[j] = (_Float16)x;
+                    lo[j] = (_Float16)(x - (float)hi[j]);
+                }
+                *reinterpret_cast<hf4*>(hiP + p * CSH + 4 * c4) = hi;
+                *reinterpret_cast<hf4*>(hiP + plane + p * CSH + 4 * c4) = lo;
             }
-            *reinterpret_cast<hf4*>(hiP + p * CSH + 4 * c4) = hi;
-            *reinterpret_cast<hf4*>(hiP + plane + p * CSH + 4 * c4) = lo;
         }
     };
-    // quad u of the accumulators: tile u / 4, registers 4 (u % 4) .. + 3 = channels co_t32 32 + 8 (u % 4) + 4 h + 0..3
-    auto quad = [&](const f16v (&acc)[TPW], int u) -> f4 {
-        const f16v& a = acc[u >> 2];
-        const int r = 4 * (u & 3);
-        return f4{a[r], a[r + 1], a[r + 2], a[r + 3]};
-    };
-    const int tbase = pp * 32 * TPW + col;  // this lane's position column of its first tile within the item
     if (item < items) {
-#pragma unroll
-        for (int e = 0; e < MAXE; ++e) fetch_e(item, e);
-#pragma unroll
-        for (int e = 0; e < MAXE; ++e) stash_e(0, e);
-        if (item + stride < items) {
-#pragma unroll
-            for (int e = 0; e < MAXE; ++e) fetch_e(item + stride, e);
-        }
+        fetch(item);
+        stash(0);
     }
     __syncthreads();
-    int buf = 0, slot = 0;
-    f4 fin[FQ], resv[FQ];   // the finished quads of the previous item (own part) and their residual
-    int64_t prev = -1;
-    float amx = 0.0f;
+    int buf = 0;
+    const int tbase = pp * 32 * TPW + col;  // this lane's position column of its first tile within the item
     for (; item < items; item += stride) {
-        const int64_t nxt = item + stride, nxt2 = item + 2 * stride;
+        const int64_t nxt = item + stride;
+        if (nxt < items) fetch(nxt);
         const _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
         const _Float16* const loP = hiP + plane;
         f16v acc[TPW];
 #pragma unroll
         for (int q = 0; q < TPW; ++q)
             acc[q] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        // vector work of this item, in chunks: MAXE stash, MAXE fetch, then per finished quad of the previous item
-        // (a) partner partials + descale + bias, (b) 4 GELUs, (c) residual + store
-        constexpr int NCH = 2 * MAXE + 3 * FQ;
-        f4 v4[FQ];
-        auto work = [&](auto cc) {
-            constexpr int c = decltype(cc)::value;
-            if constexpr (c < MAXE) {
-                if (nxt < items) stash_e(buf ^ 1, c);
-            } else if constexpr (c < 2 * MAXE) {
-                if (nxt2 < items) fetch_e(nxt2, c - MAXE);
-            } else {
-                constexpr int j = (c - 2 * MAXE) / 3, st = (c - 2 * MAXE) % 3;
-                if (prev >= 0) {
-                    const int u = kp + KS * j;
-                    if constexpr (st == 0) {
-                        f4 s = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                        for (int k = 0; k < KS; ++k) s += (k == kp) ? fin[j] : *red_at(NSLOT == 2 ? slot ^ 1 : 0, u, k);
-                        const int co = co_t32 * 32 + 8 * (u & 3) + 4 * h;
-                        const f4 bb = co < cout ? *reinterpret_cast<const f4*>(bias + co) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < 7; ++t)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v4[j][e] = fmaf(s[e], descale, bb[e]);
-                    } else if constexpr (st == 1) {
+            for (int g = 0; g < NGW; ++g)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v4[j][e] = gelu(v4[j][e]);
-                    } else {
-                        const int co = co_t32 * 32 + 8 * (u & 3) + 4 * h;
-                        const int64_t b = prev / chunks;
-                        const int l = (int)(prev - b * chunks) * PT + tbase + 32 * (u >> 2);
-                        if (co < cout) {
-                            f4 v = v4[j];
-                            if (do_res) v += resv[j];
-                            *reinterpret_cast<f4*>(out + (b * N + l) * (int64_t)cout + co) = v;
-                            amx = fmaxf(amx, amax4(v));
-                        }
-                    }
+                for (int q = 0; q < TPW; ++q) {
+                    const int off = (tbase + 32 * q + dil * t) * CSH + 16 * (g0 + g) + 8 * h;
+                    const hf8 bh = *reinterpret_cast<const hf8*>(hiP + off);
+                    const hf8 bl = *reinterpret_cast<const hf8*>(loP + off);
+                    acc[q] = mfma16(ah[t][g], bh, acc[q]);
+                    acc[q] = mfma16(ah[t][g], bl, acc[q]);
+                    acc[q] = mfma16(al[t][g], bh, acc[q]);
                 }
-            }
-        };
-        // B fragments one triple ahead
-        auto boff = [&](int tr) {
-            const int t = tr / (NGW * TPW), g = (tr / TPW) % NGW, q = tr % TPW;
-            return (tbase + 32 * q + dil * t) * CSH + 16 * (g0 + g) + 8 * h;
-        };
-        hf8 bh[2], bl[2];
-        bh[0] = *reinterpret_cast<const hf8*>(hiP + boff(0));
-        bl[0] = *reinterpret_cast<const hf8*>(loP + boff(0));
-        static_for<0, NTR>([&](auto trc) {
-            constexpr int tr = decltype(trc)::value;
-            constexpr int t = tr / (NGW * TPW), g = (tr / TPW) % NGW, q = tr % TPW;
-            if constexpr (tr + 1 < NTR) {
-                bh[(tr + 1) & 1] = *reinterpret_cast<const hf8*>(hiP + boff(tr + 1));
-                bl[(tr + 1) & 1] = *reinterpret_cast<const hf8*>(loP + boff(tr + 1));
-            }
-            acc[q] = mfma16(ah[t][g], bh[tr & 1], acc[q]);
-            acc[q] = mfma16(ah[t][g], bl[tr & 1], acc[q]);
-            acc[q] = mfma16(al[t][g], bh[tr & 1], acc[q]);
-            static_for<NCH * tr / NTR, NCH * (tr + 1) / NTR>([&](auto cc) { work(cc); });
-            __builtin_amdgcn_sched_barrier(0);
-        });
-        // hand over the quads other parts finish, keep the own ones, load their residual
-        if constexpr (KS > 1 && NSLOT == 1) __syncthreads();  // every part has read the single slot's previous sums
+        // tile q of the (co_sub, pp) group is finished by channel part q % KS
         if constexpr (KS > 1) {
 #pragma unroll
-            for (int u = 0; u < NQ; ++u)
-                if (u % KS != kp) *red_at(NSLOT == 2 ? slot : 0, u, kp) = quad(acc, u);
+            for (int q = 0; q < TPW; ++q)
+                if (q % KS != kp)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) red[((wave * RS + (RS == 1 ? 0 : q)) * 16 + r) * 64 + lane] = acc[q][r];
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < TPW; ++q)
+                if (q % KS == kp)
+#pragma unroll
+                    for (int k = 1; k < KS; ++k) {
+                        const int other = co_sub + 2 * ((kp + k) % KS + KS * pp);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            acc[q][r] += red[((other * RS + (RS == 1 ? 0 : q)) * 16 + r) * 64 + lane];
+                    }
         }
-        {
-            const int64_t b = item / chunks;
-            const int lb = (int)(item - b * chunks) * PT + tbase;
+        const int64_t b = item / chunks;
+        const int l0 = (int)(item - b * chunks) * PT;
 #pragma unroll
-            for (int j = 0; j < FQ; ++j) {
-                f4 sel = quad(acc, KS * j);
+        for (int q = 0; q < TPW; ++q) {
+            if (q % KS != kp) continue;
+            const int l = l0 + tbase + 32 * q;
 #pragma unroll
-                for (int k = 1; k < KS; ++k)
-                    if (kp == k) sel = quad(acc, KS * j + k);
-                fin[j] = sel;
-                const int u = kp + KS * j;
-                const int co = co_t32 * 32 + 8 * (u & 3) + 4 * h;
-                if (do_res && co < cout)
-                    resv[j] = *reinterpret_cast<const f4*>(res + (b * N + lb + 32 * (u >> 2)) * (int64_t)cout + co);
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int co = co_t32 * 32 + 8 * r4 + 4 * h;
+                if (co < cout) {
+                    const int64_t o = (b * N + l) * (int64_t)cout + co;
+                    const f4 bb = *reinterpret_cast<const f4*>(bias + co);
+                    f4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(acc[q][4 * r4 + e], descale, bb[e]));
+                    if (do_res) v += *reinterpret_cast<const f4*>(res + o);
+                    *reinterpret_cast<f4*>(out + o) = v;
+                    amx = fmaxf(amx, amax4(v));
+                }
             }
         }
-        prev = item;
+        if (nxt < items) stash(buf ^ 1);
         __syncthreads();
         buf ^= 1;
-        slot ^= 1;
-    }
-    // the last item's epilogue
-    if (prev >= 0) {
-        const int64_t b = prev / chunks;
-#pragma unroll
-        for (int j = 0; j < FQ; ++j) {
-            const int u = kp + KS * j;
-            f4 s = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < KS; ++k) s += (k == kp) ? fin[j] : *red_at(NSLOT == 2 ? slot ^ 1 : 0, u, k);
-            const int co = co_t32 * 32 + 8 * (u & 3) + 4 * h;
-            if (co < cout) {
-                const f4 bb = *reinterpret_cast<const f4*>(bias + co);
-                f4 v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(s[e], descale, bb[e]));
-                if (do_res) v += resv[j];
-                const int l = (int)(prev - b * chunks) * PT + tbase + 32 * (u >> 2);
-                *reinterpret_cast<f4*>(out + (b * N + l) * (int64_t)cout + co) = v;
-                amx = fmaxf(amx, amax4(v));
-            }
-        }
     }
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
 
-// LDS bytes of conv_ws2_kernel: two slab buffers (hi + lo planes) and, for KS > 1, nslot partial-sum slots
-static size_t ws2_lds_bytes(int ng, int Q, int ks, int nw, int dil, int nslot, int co) {
+// LDS bytes of conv_split_ws_kernel: two slab buffers (hi + lo planes) and, for KS > 1, the partial-sum exchange
+static size_t ws_lds_bytes(int ng, int Q, int ks, int nw, int dil) {
     const size_t slabs = (size_t)2 * 2 * (64 * Q + 6 * dil) * (16 * ng + 8) * 2;
-    const int ps = nw / co / ks, tpw = 2 * Q / ps;
-    return slabs + (ks > 1 ? (size_t)nslot * co * ps * 4 * tpw * (ks - 1) * 64 * 16 : 0);
+    const int tpw = 2 * Q / (nw / 2 / ks);
+    const int rs = (ks == 2 && tpw == 2) ? 1 : tpw;
+    return slabs + (ks > 1 ? (size_t)nw * rs * 16 * 64 * 4 : 0);
 }
 
 // ------------------------------------------------------------------------------ FC GEMM
@@ -1107,8 +1043,9 @@ extern "C" int npd_conv_destroy(npd_conv* c) {
 }
 
 static int64_t chunk_of(int64_t B) { return B < kChunk ? B : kChunk; }
-// max |activation| words of one chunk (fp16x3): conv layer i's output at [i], FC f's at [kLayers + f]
-constexpr int kAmaxSlots = 16;
+// max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
+// record kLayers + f
+constexpr int kAmaxSlots = kLayers + 3;
 
 // input4 (models.py:750, returned by convNet.forward): the (nb, N, C) activation after layers3 (+ residual) as
 // the reference's channels-first (nb, C, N).  A 64 x 64 (position x channel) tile per workgroup through LDS,
@@ -1135,7 +1072,7 @@ extern "C" int64_t npd_conv_workspace_bytes(const npd_conv* c, int64_t B) {
     if (!c || B <= 0) return 0;
     const int64_t Bc = chunk_of(B);
     // three activation buffers of (Bc, E, N) + FC1/FC2/FC3 outputs + the activation-range words (kAmaxSlots)
-    return (3 * Bc * (int64_t)c->E * c->N + Bc * 4 * (int64_t)c->N + 2 * Bc * (int64_t)c->N) * 4 + 256 + kAmaxSlots * 4;
+    return (3 * Bc * (int64_t)c->E * c->N + Bc * 4 * (int64_t)c->N + 2 * Bc * (int64_t)c->N) * 4 + 256 + (int64_t)kAmaxSlots * kAmaxWords * 4;
 }
 
 extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* logits, float* decoded, float* input4,
@@ -1175,16 +1112,16 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)fc_split_big_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kFcBigLds));
-        const void* ws[8] = {(const void*)conv_ws2_kernel<1, 1, 1, 4, 2, 2>, (const void*)conv_ws2_kernel<1, 2, 1, 4, 2, 2>,
-                             (const void*)conv_ws2_kernel<2, 1, 1, 4, 2, 2>, (const void*)conv_ws2_kernel<2, 2, 1, 4, 2, 2>,
-                             (const void*)conv_ws2_kernel<3, 1, 1, 4, 2, 2>, (const void*)conv_ws2_kernel<3, 2, 1, 4, 2, 2>,
-                             (const void*)conv_ws2_kernel<4, 1, 4, 8, 2, 2>, (const void*)conv_ws2_kernel<8, 1, 8, 8, 1, 1>};
+        const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
+                             (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
+                             (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
+                             (const void*)conv_split_ws_kernel<4, 1, 2, 4>, (const void*)conv_split_ws_kernel<8, 1, 4, 8>};
         for (const void* k : ws) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
     }
     for (int64_t b0 = 0; b0 < B; b0 += Bc) {
         const int64_t nb = (B - b0) < Bc ? (B - b0) : Bc;
-        if (split) NPD_HIP(hipMemsetAsync(amax, 0, kAmaxSlots * 4, s));
+        if (split) NPD_HIP(hipMemsetAsync(amax, 0, (size_t)kAmaxSlots * kAmaxWords * 4, s));
         // layer inputs/outputs: x (N floats per cw) -> A0 -> A1 -> ... ; block inputs kept for the residual
         const float* src = y + b0 * N;
         // buffers: cur input, output, residual source
@@ -1203,39 +1140,38 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             const int halo = 3 * L.dil;
             const size_t lds = (size_t)(L.cin == 1 ? 4 : L.cin + 4) * (64 + 2 * halo) * 4;
             dim3 grid(N / 64, (L.cout + 63) / 64, (unsigned)nb);
-            uint32_t* const am_out = split ? amax + i : nullptr;
-            const uint32_t* const am_in = i > 0 ? amax + i - 1 : nullptr;
+            uint32_t* const am_out = split ? amax + i * kAmaxWords : nullptr;
+            const uint32_t* const am_in = i > 0 ? amax + (i - 1) * kAmaxWords : nullptr;
             if (L.cin == 1)
                 hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, am_out);
             else if (split && L.dil <= 4 && (L.cin <= 64 || L.cin == 128)) {
-                // weight-stationary persistent blocks (conv_ws2_kernel), one per CU, a multiple of the channel-slice count:
-                // cin <= 48: 4 waves, 2 x 32 output channels, no channel parts; cin 64: 8 waves = 2 x 32 output channels x
-                // 4 channel parts of 16 (56 weight registers per wave), two partial-sum slots; cin 128: 8 waves = 32 output
-                // channels x 8 channel parts, one slot (two would not fit beside the slabs).  Other widths (80, 96) run the
-                // slab kernel below.
+                // weight-stationary persistent blocks: one per CU, a multiple of the 64-channel slice count.
+                // cin <= 48: 4 waves (KS 1); 64: 4 waves, 2 channel parts, two blocks per CU; 128: 8 waves, 4 channel
+                // parts, 64-position items (the 128-position slab would not fit).  Other widths (e.g. 80, 96: a 2-part
+                // split of 96 channels spills) run the slab kernel below.
                 const int ng = (L.cin + 15) / 16;
-                const int ks = ng <= 3 ? 1 : (ng == 4 ? 4 : 8);  // ng in {1, 2, 3, 4, 8}
-                const int nw = ng >= 4 ? 8 : 4;
-                const int co = ng == 8 ? 1 : 2;
+                const int ks = ng <= 3 ? 1 : (ng == 8 ? 4 : 2);  // ng in {1, 2, 3, 4, 8}
+                const int nw = ng == 8 ? 8 : 4;
                 const int Q = (ng <= 3 && N % 128 == 0) ? 2 : 1;
-                const int nslot = ng == 8 ? 1 : 2;
-                const int nslices = (L.cout + 32 * co - 1) / (32 * co);
+                const int nslices = (L.cout + 63) / 64;
                 const int64_t items = nb * (N / (64 * Q)) * nslices;
-                const size_t ls = ws2_lds_bytes(ng, Q, ks, nw, L.dil, nslot, co);
-                int64_t nblk = (int64_t)device_cu_count();
+                // cin 64: two independent 4-wave blocks per CU (67 KB of LDS each), so one block's barrier and
+                // latency waits are filled by the other's work; the others one 8- or 4-wave block per CU
+                int64_t nblk = (int64_t)device_cu_count() * (ng == 4 ? 2 : 1);
                 nblk -= nblk % nslices;
                 if (nblk > items) nblk = items;
                 if (nblk < nslices) nblk = nslices;
+                const size_t ls = ws_lds_bytes(ng, Q, ks, nw, L.dil);
                 const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff);
-#define NPD_WS(NGV, QV, KSV, NWV, NSV, COV)                                                                          \
-    hipLaunchKernelGGL((conv_ws2_kernel<NGV, QV, KSV, NWV, NSV, COV>), dim3((unsigned)nblk), dim3(64 * NWV), ls, s, in, \
-                       o, rsrc, wi, c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
-                if (ng == 8) NPD_WS(8, 1, 8, 8, 1, 1);
-                else if (ng == 4) NPD_WS(4, 1, 4, 8, 2, 2);
-                else if (ng == 1) { if (Q == 2) NPD_WS(1, 2, 1, 4, 2, 2); else NPD_WS(1, 1, 1, 4, 2, 2); }
-                else if (ng == 2) { if (Q == 2) NPD_WS(2, 2, 1, 4, 2, 2); else NPD_WS(2, 1, 1, 4, 2, 2); }
-                else { if (Q == 2) NPD_WS(3, 2, 1, 4, 2, 2); else NPD_WS(3, 1, 1, 4, 2, 2); }
+#define NPD_WS(NGV, QV, KSV, NWV)                                                                                   \
+    hipLaunchKernelGGL((conv_split_ws_kernel<NGV, QV, KSV, NWV>), dim3((unsigned)nblk), dim3(64 * NWV), ls, s, in, o, \
+                       rsrc, wi, c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
+                if (ng == 8) NPD_WS(8, 1, 4, 8);
+                else if (ng == 4) NPD_WS(4, 1, 2, 4);
+                else if (ng == 1) { if (Q == 2) NPD_WS(1, 2, 1, 4); else NPD_WS(1, 1, 1, 4); }
+                else if (ng == 2) { if (Q == 2) NPD_WS(2, 2, 1, 4); else NPD_WS(2, 1, 1, 4); }
+                else { if (Q == 2) NPD_WS(3, 2, 1, 4); else NPD_WS(3, 1, 1, 4); }
 #undef NPD_WS
             } else if (split) {
                 // positions per block 64 P: P = 2 where 128 <= N and the two fp16 slab planes fit, else 1.  (P = 4 reuses
@@ -1282,8 +1218,8 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             if (c->precision == 3) {
                 const uint16_t* wh = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][0]);
                 const uint16_t* wl = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][1]);
-                const uint32_t* am_in = amax + (f == 0 ? kLayers - 1 : kLayers + f - 1);
-                uint32_t* am_out = f < 2 ? amax + kLayers + f : nullptr;  // FC2's output feeds the fp32 LayerNorm
+                const uint32_t* am_in = amax + (f == 0 ? kLayers - 1 : kLayers + f - 1) * kAmaxWords;
+                uint32_t* am_out = f < 2 ? amax + (kLayers + f) * kAmaxWords : nullptr;  // FC2 feeds the fp32 LayerNorm
                 if (fo[f] % FB == 0) {
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
                     hipLaunchKernelGGL((fc_split_big_kernel<2, 2>), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,

@@ -142,13 +142,13 @@ def test_conv_fp16x3_error_matches_fp32_against_float64(oracle):
 def test_conv_fp16x3_shapes_vs_oracle(oracle, E, N):
     """The fp16x3 kernels at every shape family they dispatch on, against the float64 oracle on a ragged batch of more
     than one 4096-codeword chunk (seeded weights, conftest.conv_weights_from_seed): embed 64 / N 128 (weight-stationary
-    conv kernel (conv_ws2_kernel) with 32-channel groups, 128-position items; the 128 x 128 FC kernel for all three Linear
-    layers); embed 64 / N 64 (the 64-channel layer on 64-position items);
+    conv kernel with 32-channel groups, 128-position items; the 128 x 128 FC kernel for all three Linear layers); embed
+    64 / N 64 (the 64-channel layer on 64-position items);
     embed 80 / N 64 (40-channel layers = three 16-channel groups, 64-position items; the 80-channel layer on the
     slab kernel; FC1 / FC2 of 64 outputs on the 64 x 64 FC kernel); embed 96 / N 64 (48-channel layers, the 96-channel
-    layer on the slab kernel); C5 (embed 128, N 256: 64-channel layers on 8 waves in 4 channel parts, the 128-channel
-    layer on 32 output channels in 8 parts). Same bars as the golden tests: logits within 1e-5, decisions identical away
-    from zero."""
+    layer on the slab kernel); C5 (embed 128, N 256: 64-channel layers on 4-wave blocks in 2 channel parts, the
+    128-channel layer on 8 waves in 4). Same bars as the golden tests: logits within 1e-5, decisions identical away from
+    zero."""
     sd = conv_weights_from_seed(E, N, 100 + E)
     net = net_from(sd, E, N, precision="fp16x3")
     rng = np.random.default_rng(E + N)

@@ -6,7 +6,7 @@ mkdir -p gpurun_out/conv_prof
 i=0
 for lib in "$@"; do
   i=$((i + 1))
-  NPD_LIB=$(readlink -f $lib) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/conv_prof/p$i -o run -- \
+  NPD_LIB=$(readlink -f $lib) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/conv_prof/p$i -o run -- \
     python3 tools/conv_time.py 1 > gpurun_out/conv_prof/p$i.log 2>&1 || { echo "prof $lib failed"; tail -20 gpurun_out/conv_prof/p$i.log; exit 1; }
   f=$(find gpurun_out/conv_prof/p$i -name "*kernel_stats.csv" | head -1)
   echo "== $lib"; python3 -c "
