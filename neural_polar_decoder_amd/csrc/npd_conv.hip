@@ -424,9 +424,24 @@ __global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_sp
     __syncthreads();
     int buf = 0;
     const int tbase = pp * 32 * TPW + col;  // this lane's position column of its first tile within the item
+    // KS = 2, two tiles per wave (the 64-channel layers): each wave finishes tile kp; its residual quads are loaded
+    // before the MFMAs (one item of HBM latency hidden) instead of in the epilogue (measured +18 % on residual layers)
+    constexpr bool PRE_RES = KS == 2 && TPW == 2;
     for (; item < items; item += stride) {
         const int64_t nxt = item + stride;
         if (nxt < items) fetch(nxt);
+        f4 resq[4];
+        if constexpr (PRE_RES) {
+            if (do_res) {
+                const int64_t b = item / chunks;
+                const int l = (int)(item - b * chunks) * PT + tbase + 32 * kp;
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int co = co_t32 * 32 + 8 * r4 + 4 * h;
+                    if (co < cout) resq[r4] = *reinterpret_cast<const f4*>(res + (b * N + l) * (int64_t)cout + co);
+                }
+            }
+        }
         const _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
         const _Float16* const loP = hiP + plane;
         f16v acc[TPW];
@@ -480,7 +495,10 @@ __global__ __launch_bounds__(64 * NW, (NW == 4 && KS == 2) ? 2 : 1) void conv_sp
                     f4 v;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(acc[q][4 * r4 + e], descale, bb[e]));
-                    if (do_res) v += *reinterpret_cast<const f4*>(res + o);
+                    if (do_res) {
+                        if constexpr (PRE_RES) v += resq[r4];
+                        else v += *reinterpret_cast<const f4*>(res + o);
+                    }
                     *reinterpret_cast<f4*>(out + o) = v;
                     amx = fmaxf(amx, amax4(v));
                 }

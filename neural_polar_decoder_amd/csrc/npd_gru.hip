@@ -1143,30 +1143,55 @@ __device__ __forceinline__ void split_kb(const f4 (&h)[4], int kb, typename Spli
 }
 
 
+#ifndef NPD_GRU16_PF
+#define NPD_GRU16_PF 0
+#endif
+// A fragments (hi, lo) of one K block of a GEMM's NU row tiles
+template <int SPLIT, int NU>
+struct Frag16 {
+    typename SplitT<SPLIT>::V h[NU], l[NU];
+};
+template <int SPLIT, int NU>
+__device__ __forceinline__ void load_kb16(const f4* __restrict__ smem4, uint32_t wb, const int (&t)[NU], int kb,
+                                          Frag16<SPLIT, NU>& f) {
+    using V = typename SplitT<SPLIT>::V;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        f.h[u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 0));
+        if (SplitT<SPLIT>::kLo) f.l[u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 1));
+    }
+}
+
 // acc[u] += W_g[row tile t[u]] . state (both K blocks); work(IC<c>) for chunks C0 .. C0 + NCH - 1 spread evenly
-// over the 2 NU MFMA triples, one sched_barrier-fenced region per triple
+// over the 2 NU MFMA triples, one sched_barrier-fenced region per triple.  NPD_GRU16_PF: the K block 0 fragments
+// arrive in `cur`, loaded by the previous GEMM, and this GEMM loads the next one's (matrix base wbn, tiles tn) into it
+// once its own K block 0 triples have issued, so no GEMM starts on an LDS round trip.
 template <int SPLIT, int NU, int C0, int NCH, typename Work>
 __device__ __forceinline__ void gemm16i(const f4* __restrict__ smem4, uint32_t wb, const int (&t)[NU],
                                         f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
-                                        const typename SplitT<SPLIT>::V (&bl)[2], Work&& work) {
-    using V = typename SplitT<SPLIT>::V;
+                                        const typename SplitT<SPLIT>::V (&bl)[2], Frag16<SPLIT, NU>& cur,
+                                        uint32_t wbn, const int (&tn)[NU], Work&& work) {
     constexpr int NT = 2 * NU;
-    V ah[2][NU], al[2][NU];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            ah[kb][u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 0));
-            if (SplitT<SPLIT>::kLo) al[kb][u] = __builtin_bit_cast(V, frag16(smem4, wb, t[u], kb, 1));
-        }
+    Frag16<SPLIT, NU> f[2];
+    if constexpr (NPD_GRU16_PF) {
+        load_kb16<SPLIT, NU>(smem4, wb, t, 1, f[1]);
+    } else {
+        load_kb16<SPLIT, NU>(smem4, wb, t, 0, f[0]);
+        load_kb16<SPLIT, NU>(smem4, wb, t, 1, f[1]);
+    }
     asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
     static_for<0, NT>([&](auto trc) {
         constexpr int tr = decltype(trc)::value;
         constexpr int kb = tr / NU, u = tr % NU;
-        acc[u] = mfma16s(ah[kb][u], bh[kb], acc[u]);
+        const Frag16<SPLIT, NU>& F = (NPD_GRU16_PF && kb == 0) ? cur : f[kb];
+        acc[u] = mfma16s(F.h[u], bh[kb], acc[u]);
         if (SplitT<SPLIT>::kLo) {
-            acc[u] = mfma16s(ah[kb][u], bl[kb], acc[u]);
-            acc[u] = mfma16s(al[kb][u], bh[kb], acc[u]);
+            acc[u] = mfma16s(F.h[u], bl[kb], acc[u]);
+            acc[u] = mfma16s(F.l[u], bh[kb], acc[u]);
+        }
+        if constexpr (NPD_GRU16_PF && tr == NU - 1) {
+            asm volatile("" ::: "memory");
+            load_kb16<SPLIT, NU>(smem4, wbn, tn, 0, cur);
         }
         static_for<C0 + NCH * tr / NT, C0 + NCH * (tr + 1) / NT>([&](auto cc) { work(cc); });
         __builtin_amdgcn_sched_barrier(0);
@@ -1264,7 +1289,10 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
         float xb = 1.0f;
         // layer 0, hidden tile 0 of step 0: W_hh0 h0 part (the x_i column and P are added at the top of the step)
         f4 a0[3] = {zero, zero, c4(G::BHN0, 0)};
-        gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[0], T0, a0, fh, fl, nowork);
+        constexpr int T1[3] = {1, 5, 9};
+        Frag16<SPLIT, 3> cur;
+        if constexpr (NPD_GRU16_PF) load_kb16<SPLIT, 3>(smem4, wbs[0], T0, 0, cur);
+        gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[0], T0, a0, fh, fl, cur, wbs[0], T1, nowork);
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             Upd4<SPLIT> u;
@@ -1276,7 +1304,8 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                 const int T[3] = {ht, 4 + ht, 8 + ht};
                 f4 acc[3] = {fma4(xb, c4(G::C1L0, ht), P[ht]), fma4(xb, c4(G::C1L0, 4 + ht), P[4 + ht]),
                              c4(G::BHN0, ht)};
-                gemm16i<SPLIT, 3, 0, 12>(smem4, wbs[0], T, acc, fh, fl, [&](auto cc) {
+                constexpr int TN[3] = {ht < 3 ? ht + 1 : 0, ht < 3 ? 5 + ht : 4, ht < 3 ? 9 + ht : 8};
+                gemm16i<SPLIT, 3, 0, 12>(smem4, wbs[0], T, acc, fh, fl, cur, wbs[ht < 3 ? 0 : 2], TN, [&](auto cc) {
                     u.template step<decltype(cc)::value>(h0[ht - 1], ap[0], ap[1], ainp, ap[2]);
                 });
                 ainp = fma4(xb, c4(G::C1L0, 8 + ht), P[8 + ht]);
@@ -1285,13 +1314,13 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
             });
             // ================= layer 1, hidden tile 0: W_hh1 h1 beside h0 tile 3's update and the h0' split
             f4 b[3] = {c4(G::C0L1, 0), c4(G::C0L1, 4), c4(G::BHN1, 0)};
-            gemm16i<SPLIT, 3, 0, 14>(smem4, wbs[2], T0, b, gh, gl, [&](auto cc) {
+            gemm16i<SPLIT, 3, 0, 14>(smem4, wbs[2], T0, b, gh, gl, cur, wbs[1], T0, [&](auto cc) {
                 constexpr int c = decltype(cc)::value;
                 if constexpr (c < 12) u.template step<c>(h0[3], ap[0], ap[1], ainp, ap[2]);
                 else split_kb<SPLIT>(h0, c - 12, fh, fl);
             });
             f4 bi[3] = {b[0], b[1], c4(G::C0L1, 8)};
-            gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[1], T0, bi, fh, fl, nowork);
+            gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[1], T0, bi, fh, fl, cur, wbs[2], T1, nowork);
             f4 q[4] = {bi[0], bi[1], bi[2], b[2]};  // r, z, in, hn of the previous layer-1 tile
             float part = 0.0f;
             static_for<1, 4>([&](auto htc) {
@@ -1308,9 +1337,10 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                         for (int i = 0; i < 4; ++i) part = fmaf(wl[i], h1[ht - 1][i], part);
                     }
                 };
-                gemm16i<SPLIT, 3, 0, 7>(smem4, wbs[2], T, bb, gh, gl, work);
+                gemm16i<SPLIT, 3, 0, 7>(smem4, wbs[2], T, bb, gh, gl, cur, wbs[1], T, work);
                 f4 bbi[3] = {bb[0], bb[1], c4(G::C0L1, 8 + ht)};
-                gemm16i<SPLIT, 3, 7, 6>(smem4, wbs[1], T, bbi, fh, fl, work);
+                constexpr int TN[3] = {ht < 3 ? ht + 1 : 0, ht < 3 ? 5 + ht : 4, ht < 3 ? 9 + ht : 8};
+                gemm16i<SPLIT, 3, 7, 6>(smem4, wbs[1], T, bbi, fh, fl, cur, wbs[ht < 3 ? 2 : 0], TN, work);
                 q[0] = bbi[0];
                 q[1] = bbi[1];
                 q[2] = bbi[2];
@@ -1321,7 +1351,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
             a0[0] = zero;
             a0[1] = zero;
             a0[2] = c4(G::BHN0, 0);
-            gemm16i<SPLIT, 3, 0, 15>(smem4, wbs[0], T0, a0, fh, fl, [&](auto cc) {
+            gemm16i<SPLIT, 3, 0, 15>(smem4, wbs[0], T0, a0, fh, fl, cur, wbs[0], T1, [&](auto cc) {
                 constexpr int c = decltype(cc)::value;
                 if constexpr (c < 12) {
                     u.template step<c>(h1[3], q[0], q[1], q[2], q[3]);
