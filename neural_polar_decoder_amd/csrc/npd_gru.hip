@@ -498,7 +498,7 @@ __global__ __launch_bounds__(64 * NPD_GRU_WPB) void lstm_decode_kernel(const Arg
         f16v P[TT];
 #pragma unroll
         for (int t = 0; t < TT; ++t) P[t] = cvec(G::OFF_CV + t * 32);
-        {
+        if (a.y) {  // y = NULL: decoding_type y_h0 (no y input; the state starts from the y-MLP's output)
             const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
             const int ng = N / 8;
             for (int s4 = 0; s4 < ng; ++s4) {
@@ -520,6 +520,17 @@ __global__ __launch_bounds__(64 * NPD_GRU_WPB) void lstm_decode_kernel(const Arg
             c0[t] = zero;
             h1[t] = zero;
             c1[t] = zero;
+        }
+        if (a.h0) {  // y_h0: get_h0 returns (x, x) for LSTM cells (rnn_all.py:370-375): h and c both start from x
+            const float* hr = a.h0 + cwc * (int64_t)(F * L);
+#pragma unroll
+            for (int t = 0; t < HT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int f = hid_of(16 * t + i, half);
+                    h0[t][i] = c0[t][i] = hr[f * L];
+                    if constexpr (L == 2) h1[t][i] = c1[t][i] = hr[f * L + 1];
+                }
         }
         float xb = 1.0f;
         auto cell = [&](f16v& h, f16v& c, const f16v (&acc)[TT], int j) {
@@ -1850,8 +1861,8 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
             "(F = 64, 2 layers, N % 32 == 0)");
     NPD_ARG(y != nullptr || g->precision == 0 || g->img16 != nullptr,
             "npd_gru_decode: y = NULL (y_h0) needs precision 0 (fp32) or the 16-codeword split kernel");
-    NPD_ARG(g->cell == 0 || (y != nullptr && h0 == nullptr),
-            "npd_gru_decode: LSTM cells decode y_input (y given, no initial state)");
+    NPD_ARG(g->cell == 0 || ((y != nullptr) != (h0 != nullptr) && g->precision == 0),
+            "npd_gru_decode: LSTM cells decode y_input (y, no initial state) or y_h0 (initial state, no y), fp32");
     gru::Args a{};
     a.img = g->img;
     a.wy = reinterpret_cast<const gru::f4*>(g->wy);

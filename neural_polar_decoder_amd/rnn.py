@@ -22,7 +22,7 @@ class RNN_Model(nn.Module):
     out_linear_depth 1, unidirectional, no layernorm: GRU with decoding_type 'y_input' -- y_depth 0 (the CRISP
     scripts, rnn_all.py:250-253) or --use_ynn's y-MLP of N outputs feeding the GRU in place of y (rnn_all.py:1319-1320,
     :533-536) -- or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip); LSTM
-    (rnn_all.py:69) with 'y_input', fp32, hidden 32 or hidden 64 with one layer."""
+    (rnn_all.py:69) with 'y_input' or 'y_h0', fp32, hidden 32 or hidden 64 with one layer."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -104,8 +104,10 @@ class RNN_Model(nn.Module):
         common = (self.output_size == 1 and self.out_linear_depth == 1 and not self.bidirectional
                   and isinstance(self.layernorm, nn.Identity) and self.num_rnn_layers in (1, 2))
         if self.rnn_type == "LSTM":  # fp32 lstm_decode_kernel: hidden 32, or 64 with one layer (LDS-resident weights)
-            return (common and decoding_type == "y_input" and self.y_depth == 0
-                    and (self.feature_size == 32 or (self.feature_size == 64 and self.num_rnn_layers == 1)))
+            shape = self.feature_size == 32 or (self.feature_size == 64 and self.num_rnn_layers == 1)
+            if decoding_type == "y_h0":  # (h, c) both start from get_h0's x (rnn_all.py:370-375)
+                return common and shape and self._ymlp_ok(self.num_rnn_layers * self.feature_size)
+            return common and shape and decoding_type == "y_input" and self.y_depth == 0
         base = common and self.rnn_type == "GRU" and self.feature_size in (32, 64, 128, 256, 512)
         if decoding_type == "y_h0":
             return base and self._ymlp_ok(self.num_rnn_layers * self.feature_size)

@@ -514,6 +514,39 @@ def gen_gru_ynn():
              **{"w." + k: v for k, v in sd.items()})
 
 
+def gen_lstm_yh0():
+    """--rnn_type LSTM with decoding_type y_h0 (rnn_all.py:523-531; get_h0 returns (x, x) for LSTM cells, :370-375): seeded
+    PyTorch-default weights, Polar codes, reference encoder / channel at 0-4 dB, logits by a hook on net.linear."""
+    cases = [("lstm_yh0_polar_32_16_f32_l2", 32, 16, 32, 2, True, False, "selu", 64, 3, 256, 6001),
+             ("lstm_yh0_polar_64_32_f64_l1_tanh_rev", 64, 32, 64, 1, True, True, "tanh", 128, 2, 256, 6002)]
+    for name, N, K, F, L, onehot, rev, act, yh, yd, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        net = rnn_m.RNN_Model("LSTM", 1 + int(onehot), F, 1, L, N, yh, yd, act, 0.0, False)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_h0", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits, h0s = [], [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+                h0 = net.get_h0(y)[0]  # (L, B, F); the cell state starts from the same x
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+            h0s.append(h0.permute(1, 2, 0).reshape(y.shape[0], -1).numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), h0x=np.concatenate(h0s), info=info, N=N, K=K, F=F, layers=L,
+             onehot=int(onehot), rev=int(rev), activation=np.bytes_(act), y_hidden=yh, y_depth=yd,
+             **{"w." + k: v for k, v in sd.items()})
+
+
 def gen_lstm():
     """--rnn_type LSTM (rnn_all.py:69) with decoding_type y_input (rnn_all.py:532-547: hidden = (h, c) zeros): seeded
     PyTorch-default weights, Polar codes, reference encoder / channel at 0-4 dB, logits by a hook on net.linear."""
@@ -590,6 +623,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_ynn", "lstm", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_ynn", "lstm", "lstm_yh0", "conv"]
     for w in which:
         globals()["gen_" + w]()

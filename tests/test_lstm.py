@@ -30,5 +30,6 @@ def test_lstm_shapes_accepted():
     assert RNN_Model("LSTM", 66, 64, 1, 1, 64, 0, 0).fused_supported("y_input")
     assert RNN_Model("LSTM", 34, 32, 1, 2, 32, 0, 0).fused_supported("y_input")
     assert not RNN_Model("LSTM", 66, 64, 1, 2, 64, 0, 0).fused_supported("y_input")  # 192 KB of weights > LDS
-    assert not RNN_Model("LSTM", 2, 32, 1, 1, 32, 64, 2).fused_supported("y_h0")
+    assert RNN_Model("LSTM", 2, 32, 1, 1, 32, 64, 2).fused_supported("y_h0")  # y_h0: (h, c) = (x, x), round 5
+    assert not RNN_Model("LSTM", 2, 64, 1, 2, 64, 64, 2).fused_supported("y_h0")
     del torch
