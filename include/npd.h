@@ -231,8 +231,9 @@ int npd_gru_destroy(npd_gru* gru);
  * npd_gru_create for either cell of rnn_all.py:69 (--rnn_type GRU | LSTM): cell 0 = GRU (npd_gru_create), cell 1 =
  * LSTM (nn.LSTM, gates i, f, g, o; the same weight order with 4F gate rows: weight_ih_l (4F, Din_l) | weight_hh_l (4F, F)
  * | bias_ih_l (4F) | bias_hh_l (4F) per layer, then linear.weight | linear.bias).  LSTM: fp32 (precision 0), hidden 32
- * (1 or 2 layers) or 64 (1 layer: at 2 layers its weights exceed the 160 KB LDS), y_input decoding (npd_gru_decode;
- * destroy with npd_gru_destroy).
+ * (1 or 2 layers) or 64 (1 layer: at 2 layers its weights exceed the 160 KB LDS), y_input decoding (npd_gru_decode) or
+ * y_h0 decoding (npd_gru_decode_ex with y = NULL: h and c both start from h0, as get_h0 returns (x, x) for LSTM,
+ * rnn_all.py:370-375); destroy with npd_gru_destroy.
  */
 int npd_rnn_create(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
                    npd_gru** out);
@@ -251,6 +252,7 @@ int npd_gru_decode(const npd_gru* gru, const float* y, const uint8_t* is_info, i
  * the y part zero); y = NULL skips that projection.  h0: (B, F * layers) fp32 on the device, element f * layers + l =
  * layer l, hidden unit f -- get_h0's x before its reshape(-1, F, layers).permute(2, 0, 1) (rnn_all.py:362-375).
  * Precision 0, or the 16-codeword split kernel (F = 64, 2 layers, N % 32 == 0); y = NULL and h0 = NULL is an error.
+ * LSTM handles take exactly one of y (y_input) and h0 (y_h0, both states start from it), fp32.
  */
 int npd_gru_decode_ex(const npd_gru* gru, const float* y, const float* h0, const uint8_t* is_info, int reverse,
                       const float* gt, float* decoded, float* logits, int64_t B, void* stream);
