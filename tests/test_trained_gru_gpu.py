@@ -1,10 +1,12 @@
 """The fused CRISP GRU decoder (npd_gru_decode) at trained-model margins.
 
-Fixtures: tests/golden/trained_{crisp_32_16,crisp_64_32,pac_128_64}.npz -- CRISP GRUs (hidden 64, 2 layers, onehot
-y_input) trained over run_crisp.sh-shaped K + 1 curricula (tests/golden/crisp_cases.py; Polar(32,16) entirely with
-the reference's own rnn_all.py, the others' early stages on the GPU and their final stage with rnn_all.py), the
-reference's decisions and logits on 4096 words per SNR (0..4 dB) and its Monte-Carlo BER/BLER curve (2^20 words
-per SNR through RNN_decoder.decode on the CPU), by tests/golden/gen_trained.py.
+Fixtures: tests/golden/trained_{crisp_32_16,crisp_64_32}.npz -- CRISP GRUs (hidden 64, 2 layers, onehot y_input)
+trained over run_crisp.sh-shaped K + 1 curricula (tests/golden/crisp_cases.py; Polar(32,16) entirely with the
+reference's own rnn_all.py, the other's early stages on the GPU and its final stage with rnn_all.py) -- and
+trained_crisp_64_22_f512.npz, run_crisp.sh's own decoder (Polar(64,22) rev_polar, hidden 512; decoded here by the
+weight-streaming gru_wide_kernel): the reference's decisions and logits on 4096 (hidden 512: 2048) words per SNR
+(0..4 dB) and its Monte-Carlo BER/BLER curve (2^20 words per SNR, hidden 512: 2^17, through RNN_decoder.decode on the
+CPU), by tests/golden/gen_trained.py.
 
 Stated tolerance for the neural path (the north_star's "within a stated BER tolerance"):
   (a) decisions on the fixture words: >= 99.9 % of information bits and >= 99 % of codewords identical to
