@@ -51,30 +51,8 @@ struct LayerDesc {
 constexpr int kSplitSA = 4;
 
 
-// nn.GELU() (exact, erf form: x Phi(x)) without a branch: Phi(x) = 1 - q for x >= 0 and q for x < 0, where
-// q = erfc(|x| / sqrt 2) / 2 from the Chebyshev fit of erfc (Numerical Recipes, "erfcc": t exp(-z^2 + P(t)),
-// t = 1 / (1 + z / 2), fractional error < 1.2e-7 for all z >= 0) with log2 e and the 1/2 folded into P's coefficients.
-// In fp32 its absolute error against a float64 GELU is <= 3.9e-7 over [-8, 8] -- below the 4.5e-7 of
-// 0.5 x (1 + erf(x / sqrt 2)) with a correctly rounded erf, and torch's CPU fp32 GELU's 1.2e-6 -- for 2 transcendentals
-// and 17 other VALU instructions (libm erff: two regimes behind branches, ~30 instructions on each lane's path).
-__device__ __forceinline__ float gelu(float x) {
-    const float ax = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.35355339059327376220f, ax, 1.0f));  // 1 / (1 + z/2), z = |x|/sqrt2
-    // P(t) log2(e) - 1, Horner from the highest coefficient
-    float p = 0.24651730f;
-    p = fmaf(p, t, -1.18611495f);
-    p = fmaf(p, t, 2.14747446f);
-    p = fmaf(p, t, -1.63775315f);
-    p = fmaf(p, t, 0.40232158f);
-    p = fmaf(p, t, -0.26875686f);
-    p = fmaf(p, t, 0.13963006f);
-    p = fmaf(p, t, 0.53970062f);
-    p = fmaf(p, t, 1.44272920f);
-    p = fmaf(p, t, -2.82574822f);
-    const float w = ax * 0.84932180028801904272f;  // z sqrt(log2 e)
-    const float q = t * __builtin_amdgcn_exp2f(fmaf(-w, w, p));
-    return x * (x >= 0.0f ? 1.0f - q : q);
-}
+
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
 
 // The max |a| of one activation is kept in kAmaxSpread words kAmaxStride words apart (4 KB): each producing wave
 // atomicMax-es one of them (by block and wave), so tens of thousands of small blocks (layer 0) do not serialise on one

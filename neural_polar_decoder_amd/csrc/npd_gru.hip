@@ -1154,9 +1154,6 @@ __device__ __forceinline__ void split_kb(const f4 (&h)[4], int kb, typename Spli
 }
 
 
-#ifndef NPD_GRU16_PF
-#define NPD_GRU16_PF 0
-#endif
 // A fragments (hi, lo) of one K block of a GEMM's NU row tiles
 template <int SPLIT, int NU>
 struct Frag16 {
@@ -1174,33 +1171,29 @@ __device__ __forceinline__ void load_kb16(const f4* __restrict__ smem4, uint32_t
 }
 
 // acc[u] += W_g[row tile t[u]] . state (both K blocks); work(IC<c>) for chunks C0 .. C0 + NCH - 1 spread evenly
-// over the 2 NU MFMA triples, one sched_barrier-fenced region per triple.  NPD_GRU16_PF: the K block 0 fragments
-// arrive in `cur`, loaded by the previous GEMM, and this GEMM loads the next one's (matrix base wbn, tiles tn) into it
-// once its own K block 0 triples have issued, so no GEMM starts on an LDS round trip.
+// over the 2 NU MFMA triples, one sched_barrier-fenced region per triple.  The K block 0 fragments arrive in `cur`,
+// loaded by the previous GEMM, and this GEMM loads the next one's (matrix base wbn, tiles tn) into it once its own
+// K block 0 triples have issued, so no GEMM starts on an LDS round trip (measured 13.08-13.13 against 13.21-13.25 ms
+// per 2^20 words with each GEMM loading its own fragments, profiles/round5/gru16_ab.txt).
 template <int SPLIT, int NU, int C0, int NCH, typename Work>
 __device__ __forceinline__ void gemm16i(const f4* __restrict__ smem4, uint32_t wb, const int (&t)[NU],
                                         f4 (&acc)[NU], const typename SplitT<SPLIT>::V (&bh)[2],
                                         const typename SplitT<SPLIT>::V (&bl)[2], Frag16<SPLIT, NU>& cur,
                                         uint32_t wbn, const int (&tn)[NU], Work&& work) {
     constexpr int NT = 2 * NU;
-    Frag16<SPLIT, NU> f[2];
-    if constexpr (NPD_GRU16_PF) {
-        load_kb16<SPLIT, NU>(smem4, wb, t, 1, f[1]);
-    } else {
-        load_kb16<SPLIT, NU>(smem4, wb, t, 0, f[0]);
-        load_kb16<SPLIT, NU>(smem4, wb, t, 1, f[1]);
-    }
+    Frag16<SPLIT, NU> f[2];  // f[1]: this GEMM's K block 1 (K block 0 is `cur`)
+    load_kb16<SPLIT, NU>(smem4, wb, t, 1, f[1]);
     asm volatile("" ::: "memory");  // keeps the (loop-invariant) LDS fragment reads in the step loop
     static_for<0, NT>([&](auto trc) {
         constexpr int tr = decltype(trc)::value;
         constexpr int kb = tr / NU, u = tr % NU;
-        const Frag16<SPLIT, NU>& F = (NPD_GRU16_PF && kb == 0) ? cur : f[kb];
+        const Frag16<SPLIT, NU>& F = kb == 0 ? cur : f[kb];
         acc[u] = mfma16s(F.h[u], bh[kb], acc[u]);
         if (SplitT<SPLIT>::kLo) {
             acc[u] = mfma16s(F.h[u], bl[kb], acc[u]);
             acc[u] = mfma16s(F.l[u], bh[kb], acc[u]);
         }
-        if constexpr (NPD_GRU16_PF && tr == NU - 1) {
+        if constexpr (tr == NU - 1) {
             asm volatile("" ::: "memory");
             load_kb16<SPLIT, NU>(smem4, wbn, tn, 0, cur);
         }
@@ -1302,7 +1295,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
         f4 a0[3] = {zero, zero, c4(G::BHN0, 0)};
         constexpr int T1[3] = {1, 5, 9};
         Frag16<SPLIT, 3> cur;
-        if constexpr (NPD_GRU16_PF) load_kb16<SPLIT, 3>(smem4, wbs[0], T0, 0, cur);
+        load_kb16<SPLIT, 3>(smem4, wbs[0], T0, 0, cur);
         gemm16i<SPLIT, 3, 0, 0>(smem4, wbs[0], T0, a0, fh, fl, cur, wbs[0], T1, nowork);
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
