@@ -42,6 +42,7 @@ struct LayerDesc {
     // descale the accumulators by 2^-(SW + SA), SA from the input activations' range)
     int64_t soff;
     int sw;
+    int64_t soff16;  // cin 32 / 64: the same split weights as 16x16x32 A fragments (conv_ws16_kernel), else -1
 };
 
 // fp16x3: activations are split as fp16(a 2^SA) + fp16(a 2^SA - hi) when staged: SA = 4 (lo normal for |a| >= 2^-7,
@@ -49,6 +50,9 @@ struct LayerDesc {
 // (split_sa: max |a| 2^SA < 2^15, so hi cannot overflow fp16); the weights of each layer are scaled by 2^SW on the host
 // so that max |w| 2^SW is in [2^12, 2^13) (hi and lo normal for |w| >= max |w| 2^-11)
 constexpr int kSplitSA = 4;
+#ifndef NPD_CONV_WS16_OFF
+#define NPD_CONV_WS16_OFF 0
+#endif
 
 
 
@@ -61,11 +65,20 @@ constexpr int kAmaxSpread = 64;
 constexpr int kAmaxStride = 16;
 constexpr int kAmaxWords = kAmaxSpread * kAmaxStride;  // per activation
 
+// max over a full wave, returned wave-uniform: DPP within rows of 16 lanes, then the 4 row results by readlane
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+
 __device__ __forceinline__ int split_sa(const uint32_t* amax) {
     if (amax == nullptr) return kSplitSA;
-    uint32_t m = __builtin_nontemporal_load(amax + (threadIdx.x & 63) * kAmaxStride);
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, k));
+    const uint32_t m = wave_max_u32(__builtin_nontemporal_load(amax + (threadIdx.x & 63) * kAmaxStride));
     const int e = (int)((m >> 23) & 0xFFu) - 126;  // max |a| < 2^e
     return min(kSplitSA, 15 - e);
 }
@@ -74,13 +87,13 @@ __device__ __forceinline__ float amax4(const f4& v) {
     return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
 }
 
-// max over the wave of m (m >= 0), then one atomicMax of its bits (non-negative floats order as unsigned integers)
+// max over the wave of m (m >= 0, not NaN), then one atomicMax of its bits (non-negative floats order as unsigned
+// integers)
 __device__ __forceinline__ void publish_amax(uint32_t* amax, float m) {
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) m = fmaxf(m, __shfl_xor(m, k));
+    const uint32_t w = wave_max_u32(__float_as_uint(m));
     if ((threadIdx.x & 63) == 0) {
         const uint32_t blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-        atomicMax(amax + ((blk * 8 + (threadIdx.x >> 6)) % kAmaxSpread) * kAmaxStride, __float_as_uint(m));
+        atomicMax(amax + ((blk * 8 + (threadIdx.x >> 6)) % kAmaxSpread) * kAmaxStride, w);
     }
 }
 
@@ -497,6 +510,168 @@ static size_t ws_lds_bytes(int ng, int Q, int ks, int nw, int dil) {
     return slabs + (ks > 1 ? (size_t)nw * rs * 16 * 64 * 4 : 0);
 }
 
+// ------------------------------------------------------------------------------ conv layer, fp16x3, no channel parts
+// cin = 32 KB (KB = 1, 2): the weight-stationary kernel on v_mfma_f32_16x16x32_f16.  A 16-row tile of output channels
+// needs 7 taps x KB K blocks x (hi, lo) A fragments = 56 KB registers per wave (112 at cin 64), so each wave holds ALL
+// input channels of its 16 output channels -- no channel parts, no partial-sum exchange through LDS and no second
+// barrier, which is what held conv_split_ws_kernel's 64-channel layers at ~0.4 of the MFMA rate (its 32-row tiles need
+// 224 registers for all 64 channels, hence the 2 parts).  8 waves = 4 x 16 output channels (a 64-channel slice) x 2
+// position halves of a 64 Q-position item (Q 16-position tiles per wave, TPW = 2 Q).  16x16x32 operand map (lane
+// l = 16 g + c): A[row c][k 8g + j], B[k 8g + j][col c], D[row 4g + i][col c]; k of K block kb = channel 32 kb + k, so a
+// B fragment is 8 channels of one slab row: one ds_read_b128 per plane from the double-buffered hi / lo slab, and the
+// accumulator's 4 registers are 4 consecutive channels of one position (16-B epilogue stores).  The next item's slab is
+// fetched into registers before the MFMAs and split into the other buffer after them, the residual of this item
+// before them; one barrier per item.
+__device__ __forceinline__ f4 mfma16x32(const hf8& a, const hf8& b, const f4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+#ifndef NPD_WS_PROBE
+#define NPD_WS_PROBE 0  // timing probes only (wrong results): 1 no MFMAs, 2 no activation loads, 3 no slab stores
+#endif
+template <int KB, int Q>
+__global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                           const float* __restrict__ res, const f4* __restrict__ wimg,
+                                                           const float* __restrict__ bias, int cout, int N, int dil,
+                                                           int do_res, int sw, const uint32_t* __restrict__ amax_in,
+                                                           uint32_t* __restrict__ amax_out, int64_t nb, int nslices) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 slab16[];
+    constexpr int NT = 512;
+    constexpr int CIN = 32 * KB;
+    constexpr int PT = 64 * Q;        // positions per item
+    constexpr int C4P = CIN / 4;      // float4 channel groups per staged row
+    constexpr int CSH = CIN + 8;      // fp16 row stride of the LDS slab (conflict-free ds_read_b128)
+    constexpr int MAXE = ((PT + 24) * C4P + NT - 1) / NT;
+    constexpr int TPW = 2 * Q;        // 16-position tiles per wave
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const int co16 = wave & 3, pp = wave >> 2;
+    const int halo = 3 * dil;
+    const int W = PT + 2 * halo;
+    const int plane = W * CSH;
+    const int slice = blockIdx.x % nslices;
+    const int t16 = slice * 4 + co16;  // 16-channel output tile
+    const int sa = split_sa(amax_in);
+    const float sa_scale = __builtin_ldexpf(1.0f, sa), descale = __builtin_ldexpf(1.0f, -(sw + sa));
+    hf8 ah[7][KB], al[7][KB];
+    {
+        const f4* wq = wimg + (int64_t)t16 * 7 * KB * 128 + lane;
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                ah[t][kb] = __builtin_bit_cast(hf8, wq[(t * KB + kb) * 128]);
+                al[t][kb] = __builtin_bit_cast(hf8, wq[(t * KB + kb) * 128 + 64]);
+            }
+    }
+    const int chunks = N / PT;
+    const int items = (int)nb * chunks;
+    const int stride = gridDim.x / nslices;
+    int item = blockIdx.x / nslices;
+    f4 pre[MAXE];
+    auto fetch = [&](int it) {
+        const int b = it / chunks;
+        const int l0 = (it - b * chunks) * PT;
+        const f4* inb = reinterpret_cast<const f4*>(in + (int64_t)b * N * CIN);
+#pragma unroll
+        for (int e = 0; e < MAXE; ++e) {
+            const int idx = tid + NT * e;
+            const int p = idx / C4P, c4 = idx - p * C4P;
+            const int l = l0 - halo + p;
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (NPD_WS_PROBE != 2 && p < W && l >= 0 && l < N) v = inb[(int64_t)l * C4P + c4];
+            pre[e] = v;
+        }
+    };
+    auto stash = [&](int buf) {
+        _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
+#pragma unroll
+        for (int e = 0; e < MAXE; ++e) {
+            const int idx = tid + NT * e;
+            const int p = idx / C4P, c4 = idx - p * C4P;
+            if (p < W) {
+                hf4 hi, lo;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float x = pre[e][j] * sa_scale;
+                    hi[j] = (_Float16)x;
+                    lo[j] = (_Float16)(x - (float)hi[j]);
+                }
+                if (NPD_WS_PROBE == 3) {
+                    if ((float)hi[0] + (float)lo[3] == 12345.f) hiP[tid] = hi[1];
+                    continue;
+                }
+                *reinterpret_cast<hf4*>(hiP + p * CSH + 4 * c4) = hi;
+                *reinterpret_cast<hf4*>(hiP + plane + p * CSH + 4 * c4) = lo;
+            }
+        }
+    };
+    if (item < items) {
+        fetch(item);
+        stash(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    const int tbase = pp * 16 * TPW + col;  // this lane's position column of its first tile within the item
+    const int co = t16 * 16 + 4 * g;        // the lane's 4 output channels
+    const bool co_ok = co < cout;
+    const f4 bb = co_ok ? *reinterpret_cast<const f4*>(bias + co) : f4{0.f, 0.f, 0.f, 0.f};
+    float amx = 0.0f;
+    for (; item < items; item += stride) {
+        const int nxt = item + stride;
+        if (nxt < items) fetch(nxt);
+        const int b = item / chunks;
+        const int64_t row0 = (int64_t)b * N + (item - b * chunks) * PT + tbase;  // output row of tile 0
+        f4 resv[TPW];
+        if (do_res && co_ok) {
+#pragma unroll
+            for (int q = 0; q < TPW; ++q) resv[q] = *reinterpret_cast<const f4*>(res + (row0 + 16 * q) * cout + co);
+        }
+        const _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
+        const _Float16* const loP = hiP + plane;
+        f4 acc[TPW];
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                for (int q = 0; q < TPW; ++q) {
+                    const int off = (tbase + 16 * q + dil * t) * CSH + 32 * kb + 8 * g;
+                    const hf8 bh = *reinterpret_cast<const hf8*>(hiP + off);
+                    const hf8 bl = *reinterpret_cast<const hf8*>(loP + off);
+                    if (NPD_WS_PROBE == 1) {
+                        acc[q][0] += (float)bh[t] + (float)bl[kb] + (float)ah[t][kb][q] + (float)al[t][kb][q + 1];
+                        continue;
+                    }
+                    acc[q] = mfma16x32(ah[t][kb], bh, acc[q]);
+                    acc[q] = mfma16x32(ah[t][kb], bl, acc[q]);
+                    acc[q] = mfma16x32(al[t][kb], bh, acc[q]);
+                }
+        if (co_ok) {
+#pragma unroll
+            for (int q = 0; q < TPW; ++q) {
+                f4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(acc[q][e], descale, bb[e]));
+                if (do_res) v += resv[q];
+                *reinterpret_cast<f4*>(out + (row0 + 16 * q) * cout + co) = v;
+                amx = fmaxf(amx, amax4(v));
+            }
+        }
+        if (nxt < items) stash(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    if (amax_out != nullptr) publish_amax(amax_out, amx);
+}
+
+static size_t ws16_lds_bytes(int kb, int Q, int dil) {
+    return (size_t)2 * 2 * (64 * Q + 6 * dil) * (32 * kb + 8) * 2;
+}
+
 // ------------------------------------------------------------------------------ FC GEMM
 // out[m][j] = act(sum_k X[m][k] * Wt[j][k] + bias[j]);  block tile 64 (m) x 64 (j), K step 32.
 // LDS rows of stride GK + 4 (16-B aligned; 32 rows read with ds_read_b128 at one k offset hit every bank
@@ -673,7 +848,7 @@ __global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__
 // block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords -- is read from HBM once, not once per
 // column tile.  LDS 144 KB (dynamic).
 constexpr int FB = 128;
-constexpr int FD = 3;
+
 // LDS row stride of the 128-row planes: 72 halfs (144 B = 36 banks, as the conv slabs) -- the 64 x 64 kernel's 40
 // (80 B = 20 banks) left a third of this kernel's LDS cycles bank-conflicted (PMC SQ_LDS_BANK_CONFLICT /
 // SQ_LDS_IDX_ACTIVE, profiles/round4/pmc_conv_summary.json); removing them moved the kernel by 2 % (405 vs 408-414 us
@@ -681,8 +856,34 @@ constexpr int FD = 3;
 constexpr int GSB = 72;
 constexpr size_t kFcBigLds = (size_t)2 * 4 * FB * GSB * 2;
 
-// WM x WN waves over the 128 x 128 tile, each (128 / WM) x (128 / WN) = TM x TN MFMA tiles of 32 x 32
-template <int WM, int WN>
+// WM x WN waves over the 128 x 128 tile, each (128 / WM) x (128 / WN) = TM x TN MFMA tiles of 32 x 32.  K blocks of
+// GKT (32 or 64) run through an FDT-deep register ring; a step is ONE basic block (the ring's prefetch index is clamped
+// at the tail instead of branched on, the last step's spare stash lands in the buffer nobody reads any more), and the
+// split / store of block kb + 1 is cut into GKT / 16 parts issued beside the MFMAs of block kb's k-steps, whose
+// fragments are read one k-step ahead -- so the compiler can fill the MFMA gaps with the split and the LDS stores
+// instead of running them after the MFMAs, at one wave per SIMD.  The activation scale's amax words are loaded before
+// the first K blocks and reduced after them.
+#ifndef NPD_FC_GK
+#define NPD_FC_GK 32
+#endif
+#ifndef NPD_FC_FD
+#define NPD_FC_FD 3
+#endif
+#ifndef NPD_FC_PROBE
+#define NPD_FC_PROBE 0  // timing probes only (wrong results): 1 no MFMAs, 2 no loads, 3 no LDS stores
+#endif
+#ifndef NPD_FC_SG
+#define NPD_FC_SG 0
+#endif
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+template <int WM, int WN, int GKT, int FDT>
 __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float* __restrict__ X,
                                                                     const uint16_t* __restrict__ Whi,
                                                                     const uint16_t* __restrict__ Wlo,
@@ -691,10 +892,13 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
                                                                     int act, int sw, const uint32_t* __restrict__ amax_in,
                                                                     uint32_t* __restrict__ amax_out) {
     constexpr int NT = 64 * WM * WN;
-    const int sa = split_sa(amax_in);
-    const float sa_scale = __builtin_ldexpf(1.0f, sa), descale = __builtin_ldexpf(1.0f, -(sw + sa));
     constexpr int TM = FB / 32 / WM, TN = FB / 32 / WN;
-    constexpr int UA = 1024 / NT, UB = 512 / NT;  // f4 loads per thread: A (128 x 32 fp32), each B plane
+    constexpr int ST = GKT / 16;                                 // k-steps per K block
+    constexpr int A4 = GKT / 4, B8 = GKT / 8;                    // f4 per A row, 16-B pieces per B row
+    constexpr int UA = FB * A4 / NT, UB = FB * B8 / NT;          // per thread: A f4 loads, B loads per plane
+    constexpr int PA = UA / ST, PB = UB / ST;                    // per stash part
+    static_assert(UA % ST == 0 && UB % ST == 0 && GKT + 8 <= GSB, "FC tile");
+    const uint32_t am_raw = amax_in != nullptr ? __builtin_nontemporal_load(amax_in + (threadIdx.x & 63) * kAmaxStride) : 0u;
     extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [buf][plane A hi, A lo, B hi, B lo][128][GSB]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -707,12 +911,19 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
     const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
     const int wm = wave % WM, wn = wave / WM;
     constexpr int PL = FB * GSB;  // halfs per plane
-    f4 ra[FD][UA], rbh[FD][UB], rbl[FD][UB];
+    f4 ra[FDT][UA], rbh[FDT][UB], rbl[FDT][UB];
     auto fetch = [&](int slot, int k0) {
+        if (NPD_FC_PROBE == 2) {
+#pragma unroll
+            for (int u = 0; u < UA; ++u) ra[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
+#pragma unroll
+            for (int u = 0; u < UB; ++u) rbh[slot][u] = rbl[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < UA; ++u) {
             const int idx = tid + NT * u;
-            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            const int r = idx / A4, c4 = (idx % A4) * 4;
             int mr = m0 + r;
             if (mr >= M) mr = M - 1;
             ra[slot][u] = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
@@ -720,17 +931,28 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const int idx = tid + NT * u;
-            const int r = idx >> 2, c8 = (idx & 3) * 8;
+            const int r = idx / B8, c8 = (idx % B8) * 8;
             rbh[slot][u] = *reinterpret_cast<const f4*>(Whi + (int64_t)(j0 + r) * K + k0 + c8);
             rbl[slot][u] = *reinterpret_cast<const f4*>(Wlo + (int64_t)(j0 + r) * K + k0 + c8);
         }
     };
-    auto stash = [&](int slot, int buf) {
+    float sa_scale = 1.0f;
+    auto stash = [&](int slot, int buf, int part) {
         _Float16* const base = smb + (size_t)buf * 4 * PL;
+        if (NPD_FC_PROBE == 3) {
+            float q = 0.f;
 #pragma unroll
-        for (int u = 0; u < UA; ++u) {
+            for (int v = 0; v < PA; ++v) q += ra[slot][part * PA + v][0] + ra[slot][part * PA + v][3];
+#pragma unroll
+            for (int v = 0; v < PB; ++v) q += rbh[slot][part * PB + v][0] + rbl[slot][part * PB + v][1];
+            if (q == 12345.f) base[tid] = (_Float16)q;
+            return;
+        }
+#pragma unroll
+        for (int v = 0; v < PA; ++v) {
+            const int u = part * PA + v;
             const int idx = tid + NT * u;
-            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            const int r = idx / A4, c4 = (idx % A4) * 4;
             hf4 hi, lo;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -742,9 +964,10 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
             *reinterpret_cast<hf4*>(base + PL + r * GSB + c4) = lo;
         }
 #pragma unroll
-        for (int u = 0; u < UB; ++u) {
+        for (int v = 0; v < PB; ++v) {
+            const int u = part * PB + v;
             const int idx = tid + NT * u;
-            const int r = idx >> 2, c8 = (idx & 3) * 8;
+            const int r = idx / B8, c8 = (idx % B8) * 8;
             *reinterpret_cast<f4*>(base + 2 * PL + r * GSB + c8) = rbh[slot][u];
             *reinterpret_cast<f4*>(base + 3 * PL + r * GSB + c8) = rbl[slot][u];
         }
@@ -755,52 +978,71 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
 #pragma unroll
         for (int b = 0; b < TN; ++b)
             acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const int nk = K / GK;
+    const int nk = K / GKT;
     const int ar = (wm * 32 * TM + col) * GSB + 8 * h, br = (wn * 32 * TN + col) * GSB + 8 * h;
-    // K block kb lives in ring slot kb % FD until it is stashed into LDS buffer kb & 1
-    fetch(0, 0);
+    // K block kb lives in ring slot kb % FDT until it is stashed into LDS buffer kb & 1
 #pragma unroll
-    for (int d = 1; d < FD; ++d)
-        if (d < nk) fetch(d, d * GK);
-    stash(0, 0);
+    for (int d = 0; d < FDT; ++d) fetch(d, min(d, nk - 1) * GKT);
+    const int sa = amax_in != nullptr ? min(kSplitSA, 15 - ((int)((wave_max_u32(am_raw) >> 23) & 0xFFu) - 126)) : kSplitSA;
+    sa_scale = __builtin_ldexpf(1.0f, sa);
+    const float descale = __builtin_ldexpf(1.0f, -(sw + sa));
+#pragma unroll
+    for (int p = 0; p < ST; ++p) stash(0, 0, p);
     __syncthreads();
+    struct Frags {
+        hf8 ah[TM], al[TM], bh[TN], bl[TN];
+    };
+    auto read = [&](const _Float16* cb, int st, Frags& f) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+            f.ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GSB + 16 * st);
+            f.al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GSB + 16 * st);
+        }
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+            f.bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GSB + 16 * st);
+            f.bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GSB + 16 * st);
+        }
+    };
     auto step = [&](int kb, auto slot_c) {
-        constexpr int SL = decltype(slot_c)::value;  // kb % FD
+        constexpr int SL = decltype(slot_c)::value;  // kb % FDT
         const _Float16* const cb = smb + (size_t)(kb & 1) * 4 * PL;
-        if (kb + FD < nk) fetch(SL, (kb + FD) * GK);  // slot SL was stashed at step kb - 1
+        fetch(SL, min(kb + FDT, nk - 1) * GKT);  // slot SL was stashed at step kb - 1
+        Frags f[2];
+        read(cb, 0, f[0]);
 #pragma unroll
-        for (int st = 0; st < GK / 16; ++st) {
-            hf8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-            for (int t = 0; t < TM; ++t) {
-                ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GSB + 16 * st);
-                al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GSB + 16 * st);
-            }
-#pragma unroll
-            for (int t = 0; t < TN; ++t) {
-                bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GSB + 16 * st);
-                bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GSB + 16 * st);
-            }
+        for (int st = 0; st < ST; ++st) {
+            if (st + 1 < ST) read(cb, st + 1, f[(st + 1) & 1]);
+            const Frags& c = f[st & 1];
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
                 for (int b = 0; b < TN; ++b) {
-                    acc[a][b] = mfma16(ah[a], bh[b], acc[a][b]);
-                    acc[a][b] = mfma16(ah[a], bl[b], acc[a][b]);
-                    acc[a][b] = mfma16(al[a], bh[b], acc[a][b]);
+                    if (NPD_FC_PROBE == 1) {
+                        acc[a][b][0] += (float)c.ah[a][0] + (float)c.bh[b][1] + (float)c.al[a][2] + (float)c.bl[b][3];
+                        continue;
+                    }
+                    acc[a][b] = mfma16(c.ah[a], c.bh[b], acc[a][b]);
+                    acc[a][b] = mfma16(c.ah[a], c.bl[b], acc[a][b]);
+                    acc[a][b] = mfma16(c.al[a], c.bh[b], acc[a][b]);
                 }
+            stash((SL + 1) % FDT, (kb + 1) & 1, st);
+#if NPD_FC_SG
+#pragma unroll
+            for (int i = 0; i < TM * TN * 3; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                if (i % 3 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            }
+#endif
         }
-        if (kb + 1 < nk) stash((SL + 1) % FD, (kb + 1) & 1);
         __syncthreads();
     };
     int kb = 0;
-    for (; kb + FD <= nk; kb += FD) {
-        step(kb, std::integral_constant<int, 0>{});
-        step(kb + 1, std::integral_constant<int, 1>{});
-        step(kb + 2, std::integral_constant<int, 2>{});
-    }
-    if (kb < nk) step(kb, std::integral_constant<int, 0>{});
-    if (kb + 1 < nk) step(kb + 1, std::integral_constant<int, 1>{});
+    for (; kb + FDT <= nk; kb += FDT) static_for<0, FDT>([&](auto i) { step(kb + i.value, i); });
+    static_for<0, FDT>([&](auto i) {
+        if (kb + i.value < nk) step(kb + i.value, i);
+    });
     float amx = 0.0f;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -821,6 +1063,247 @@ __global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float*
         }
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
+#define FC_BIG fc_split_big_kernel<2, 2, NPD_FC_GK, NPD_FC_FD>
+#define FC_BIG_32 fc_split_big_kernel<2, 2, 32, 3>
+
+// The same 128 x 128 fp16x3 tile with the waves specialised (512 threads, two waves per SIMD): waves 0-3 only read
+// fragments and issue MFMAs (64 x 64 each, as above); waves 4-7 only load, split and store.  The loaders keep FDL K
+// blocks in flight in their registers and fill an NS-slot LDS ring two blocks ahead of the MFMA waves; one barrier per
+// K block.  With one wave per SIMD the split, the LDS stores and the waits for HBM sat between a SIMD's MFMAs
+// (fc_split_big_kernel's MFMA-free timing probe ran 94 % as long as the kernel); here they run on the SIMD's other wave.
+#ifndef NPD_FC_WSP
+#define NPD_FC_WSP 1
+#endif
+#ifndef NPD_FC_FDL
+#define NPD_FC_FDL 3
+#endif
+#ifndef NPD_FC_PADEXP
+#define NPD_FC_PADEXP 0
+#endif
+#ifndef NPD_FC_PANELEXP
+#define NPD_FC_PANELEXP 0
+#endif
+// (rows, K) row-major -> [K / 32][rows][32] panels (experiment copies)
+__global__ void panel32_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int K) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)rows * K / 4) return;
+    const int64_t m = i / (K / 4);
+    const int k = (int)(i % (K / 4)) * 4;
+    *reinterpret_cast<f4*>(dst + ((int64_t)(k / 32) * rows + m) * 32 + k % 32) = *reinterpret_cast<const f4*>(src + m * K + k);
+}
+__global__ void panel16_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, int rows, int K) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)rows * K / 8) return;
+    const int64_t m = i / (K / 8);
+    const int k = (int)(i % (K / 8)) * 8;
+    *reinterpret_cast<f4*>(dst + ((int64_t)(k / 32) * rows + m) * 32 + k % 32) = *reinterpret_cast<const f4*>(src + m * K + k);
+}
+// workgroup barrier that orders LDS only: a __syncthreads() also waits for every global load in flight (vmcnt(0)),
+// which would drain the loaders' register ring at each K block
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+constexpr int GSW = 40;  // LDS row stride (halfs) of the 32-wide K blocks: 80 B, conflict-free ds_read_b128 rows
+constexpr int kWspSlots = 3;
+constexpr size_t kFcWspLds = (size_t)kWspSlots * 4 * FB * GSW * 2;
+template <int FDL>
+__global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Whi,
+                                                              const uint16_t* __restrict__ Wlo,
+                                                              const float* __restrict__ bias, float* __restrict__ out,
+                                                              int M, int K, int Nout, int act, int sw,
+                                                              const uint32_t* __restrict__ amax_in,
+                                                              uint32_t* __restrict__ amax_out, int lda, int ldb) {
+    constexpr int GKT = 32, NS = kWspSlots;
+    static_assert(FDL >= 2 && FDL % NS == 0, "the prologue stashes two K blocks; LDS slots repeat with the ring");
+    constexpr int NL = 256;                            // loader threads
+    constexpr int A4 = GKT / 4, B8 = GKT / 8;          // f4 per A row, 16-B pieces per B row
+    constexpr int UA = FB * A4 / NL, UB = FB * B8 / NL;  // 4, 2
+    constexpr int TM = 2, TN = 2;
+    constexpr int PL = FB * GSW;  // halfs per plane
+    const uint32_t am_raw = amax_in != nullptr ? __builtin_nontemporal_load(amax_in + (threadIdx.x & 63) * kAmaxStride) : 0u;
+    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [slot][A hi, A lo, B hi, B lo][128][GSW]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const bool loader = wave >= 4;
+    const int gx = Nout / FB;
+    const int total = gridDim.x;
+    int lin = blockIdx.x;
+    if ((total & 7) == 0) lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
+    const int nk = K / GKT;
+    const int sa = amax_in != nullptr ? min(kSplitSA, 15 - ((int)((wave_max_u32(am_raw) >> 23) & 0xFFu) - 126)) : kSplitSA;
+    const float sa_scale = __builtin_ldexpf(1.0f, sa), descale = __builtin_ldexpf(1.0f, -(sw + sa));
+    float amx = 0.0f;
+    if (loader) {
+        const int lt = tid - 256;
+        // per-lane byte offsets (fixed for the launch) against wave-uniform K-block bases: one 32-bit address register
+        // per load, no 64-bit address arithmetic per K block
+        uint32_t offA[UA], offB[UB], ldsA[UA], ldsB[UB];
+#pragma unroll
+        for (int u = 0; u < UA; ++u) {
+            const int idx = lt + NL * u;
+            const int r = idx / A4, c4 = (idx % A4) * 4;
+            const int mr = min(m0 + r, M - 1);
+            offA[u] = (uint32_t)((lda ? (int64_t)mr * lda + c4 : (int64_t)mr * GKT + c4) * 4);
+            ldsA[u] = (uint32_t)(r * GSW + c4);
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            const int idx = lt + NL * u;
+            const int r = idx / B8, c8 = (idx % B8) * 8;
+            offB[u] = (uint32_t)((ldb ? (int64_t)(j0 + r) * ldb + c8 : (int64_t)(j0 + r) * GKT + c8) * 2);
+            ldsB[u] = (uint32_t)(r * GSW + c8);
+        }
+        f4 ra[FDL][UA], rbh[FDL][UB], rbl[FDL][UB];
+        auto fetch = [&](int slot, int kb) {
+            const int k0 = min(kb, nk - 1) * GKT;
+            if (NPD_FC_PROBE == 2) {
+#pragma unroll
+                for (int u = 0; u < UA; ++u) ra[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
+#pragma unroll
+                for (int u = 0; u < UB; ++u) rbh[slot][u] = rbl[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
+                return;
+            }
+            // lda / ldb 0: panel-major operand, [K / 32][rows][32]
+            const char* const xk = reinterpret_cast<const char*>(X) + (lda ? (size_t)k0 : (size_t)k0 * M) * 4;
+            const char* const hk = reinterpret_cast<const char*>(Whi) + (ldb ? (size_t)k0 : (size_t)k0 * Nout) * 2;
+            const char* const lk = reinterpret_cast<const char*>(Wlo) + (ldb ? (size_t)k0 : (size_t)k0 * Nout) * 2;
+#pragma unroll
+            for (int u = 0; u < UA; ++u) ra[slot][u] = *reinterpret_cast<const f4*>(xk + offA[u]);
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                rbh[slot][u] = *reinterpret_cast<const f4*>(hk + offB[u]);
+                rbl[slot][u] = *reinterpret_cast<const f4*>(lk + offB[u]);
+            }
+        };
+        auto stash = [&](int slot, auto lds_slot) {
+            _Float16* const base = smb + (size_t)decltype(lds_slot)::value * 4 * PL;
+#pragma unroll
+            for (int u = 0; u < UA; ++u) {
+                hf4 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = ra[slot][u][e] * sa_scale;
+                    hi[e] = (_Float16)x;
+                    lo[e] = (_Float16)(x - (float)hi[e]);
+                }
+                *reinterpret_cast<hf4*>(base + ldsA[u]) = hi;
+                *reinterpret_cast<hf4*>(base + PL + ldsA[u]) = lo;
+            }
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                *reinterpret_cast<f4*>(base + 2 * PL + ldsB[u]) = rbh[slot][u];
+                *reinterpret_cast<f4*>(base + 3 * PL + ldsB[u]) = rbl[slot][u];
+            }
+        };
+        // block b lives in register slot b % FDL from its fetch to its stash into LDS slot b % NS
+        static_for<0, FDL>([&](auto i) { fetch(i.value, i.value); });
+        stash(0, std::integral_constant<int, 0>{});
+        stash(1, std::integral_constant<int, 1>{});
+        fetch(0, FDL);
+        fetch(1, FDL + 1);
+        lds_barrier();
+        // step k: the MFMA waves read slot k % NS; the loaders stash block k + 2 and fetch block k + 2 + FDL
+        int kb = 0;
+        for (; kb + FDL <= nk; kb += FDL)
+            static_for<0, FDL>([&](auto i) {
+                constexpr int RS = (i.value + 2) % FDL;
+                stash(RS, std::integral_constant<int, (i.value + 2) % NS>{});
+                fetch(RS, kb + i.value + 2 + FDL);
+                lds_barrier();
+            });
+        static_for<0, FDL>([&](auto i) {
+            if (kb + i.value < nk) {
+                constexpr int RS = (i.value + 2) % FDL;
+                stash(RS, std::integral_constant<int, (i.value + 2) % NS>{});
+                lds_barrier();
+            }
+        });
+    } else {
+        __builtin_amdgcn_s_setprio(1);
+        const int h = lane >> 5, col = lane & 31;
+        const int wm = wave & 1, wn = wave >> 1;
+        f16v acc[TM][TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const int ar = (wm * 32 * TM + col) * GSW + 8 * h, br = (wn * 32 * TN + col) * GSW + 8 * h;
+        struct Frags {
+            hf8 ah[TM], al[TM], bh[TN], bl[TN];
+        };
+        auto read = [&](int slot, int st, Frags& f) {
+            const _Float16* const cb = smb + (size_t)slot * 4 * PL + 16 * st;
+#pragma unroll
+            for (int t = 0; t < TM; ++t) {
+                f.ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GSW);
+                f.al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GSW);
+            }
+#pragma unroll
+            for (int t = 0; t < TN; ++t) {
+                f.bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GSW);
+                f.bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GSW);
+            }
+        };
+        Frags f[2];
+        lds_barrier();
+        read(0, 0, f[0]);
+        // slot (kb + 1) % NS was complete at the barrier that ended step kb - 1, so its first k-step's fragments are
+        // read during step kb's MFMAs (the loaders write slot (kb + 2) % NS meanwhile)
+        auto step = [&](auto slot_c) {
+            constexpr int SL = decltype(slot_c)::value;  // kb % NS
+#pragma unroll
+            for (int st = 0; st < GKT / 16; ++st) {
+                if (st + 1 < GKT / 16)
+                    read(SL, st + 1, f[(st + 1) & 1]);
+                else
+                    read((SL + 1) % NS, 0, f[(st + 1) & 1]);
+                const Frags& c = f[st & 1];
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b) {
+                        if (NPD_FC_PROBE == 1) {
+                            acc[a][b][0] += (float)c.ah[a][0] + (float)c.bh[b][1] + (float)c.al[a][2] + (float)c.bl[b][3];
+                            continue;
+                        }
+                        acc[a][b] = mfma16(c.ah[a], c.bh[b], acc[a][b]);
+                        acc[a][b] = mfma16(c.ah[a], c.bl[b], acc[a][b]);
+                        acc[a][b] = mfma16(c.al[a], c.bh[b], acc[a][b]);
+                    }
+            }
+            lds_barrier();
+        };
+        int kb = 0;
+        for (; kb + NS <= nk; kb += NS) static_for<0, NS>([&](auto i) { step(i); });
+        static_for<0, NS>([&](auto i) {
+            if (kb + i.value < nk) step(i);
+        });
+        __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const int j = j0 + wn * 32 * TN + 32 * b + col;
+                const float bj = bias[j];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * 32 * TM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (m < M) {
+                        float v = fmaf(acc[a][b][r], descale, bj);
+                        if (act) v = gelu(v);
+                        out[(int64_t)m * Nout + j] = v;
+                        amx = fmaxf(amx, fabsf(v));
+                    }
+                }
+            }
+    }
+    if (amax_out != nullptr) publish_amax(amax_out, amx);
+}
+#define FC_WSP fc_split_wsp_kernel<NPD_FC_FDL>
 
 // ------------------------------------------------------------------------------ LayerNorm + sign
 __global__ __launch_bounds__(256) void layernorm_sign_kernel(const float* __restrict__ x, const float* __restrict__ g,
@@ -907,6 +1390,7 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
         conv_spec(E, i, ci, co, d, r);
         LayerDesc& L = c->layers[i];
         L.cin = ci; L.cout = co; L.dil = d; L.res = r;
+        L.soff16 = -1;
         L.ksteps = (7 * ci + 1) / 2;
         // pad channel tiles to 64 so every (64-channel) block has two 32-row MFMA tiles
         const int co_pad = ((co + 63) / 64) * 64;
@@ -964,6 +1448,30 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
                                 memcpy(&u16[e], &hi, 2);
                                 memcpy(&u16[e + 64 * 8], &lo, 2);
                             }
+            L.soff16 = -1;
+            if (ci == 32 || ci == 64) {
+                // conv_ws16_kernel A fragments [t16][tap][kb][part hi/lo][lane][8 x fp16]: 16x16x32 map, lane l = 16 g + r,
+                // element j = W[row 16 t16 + r][32 kb + 8 g + j][t] x 2^SW
+                const int kbn = ci / 32;
+                while (img.size() % 4) img.push_back(0.0f);
+                L.soff16 = (int64_t)img.size();
+                const size_t m16 = (size_t)(co_pad / 16) * 7 * kbn * 2 * 64 * 8;
+                img.resize(img.size() + m16 / 2, 0.0f);
+                uint16_t* v16 = reinterpret_cast<uint16_t*>(img.data() + L.soff16);
+                for (int t16 = 0; t16 < co_pad / 16; ++t16)
+                    for (int t = 0; t < 7; ++t)
+                        for (int kb = 0; kb < kbn; ++kb)
+                            for (int l = 0; l < 64; ++l)
+                                for (int j = 0; j < 8; ++j) {
+                                    const int row = 16 * t16 + (l & 15), cc = 32 * kb + 8 * (l >> 4) + j;
+                                    const float v = row < co ? w[((int64_t)row * ci + cc) * 7 + t] * sc : 0.0f;
+                                    const _Float16 hi = (_Float16)v;
+                                    const _Float16 lo = (_Float16)(v - (float)hi);
+                                    const size_t e = ((((size_t)(t16 * 7 + t) * kbn + kb) * 2) * 64 + l) * 8 + j;
+                                    memcpy(&v16[e], &hi, 2);
+                                    memcpy(&v16[e + 64 * 8], &lo, 2);
+                                }
+            }
         }
         p += (int64_t)co * ci * 7;
         L.boff = (int64_t)img.size();
@@ -1106,13 +1614,17 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
-        NPD_HIP(hipFuncSetAttribute((const void*)fc_split_big_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kFcBigLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_BIG, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcBigLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_BIG_32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcBigLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
         const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<4, 1, 2, 4>, (const void*)conv_split_ws_kernel<8, 1, 4, 8>};
         for (const void* k : ws) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        const void* w16[4] = {(const void*)conv_ws16_kernel<1, 1>, (const void*)conv_ws16_kernel<1, 2>,
+                              (const void*)conv_ws16_kernel<2, 1>, (const void*)conv_ws16_kernel<2, 2>};
+        for (const void* k : w16) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
     }
     for (int64_t b0 = 0; b0 < B; b0 += Bc) {
@@ -1141,7 +1653,26 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             if (L.cin == 1)
                 hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, am_out);
-            else if (split && L.dil <= 4 && (L.cin <= 64 || L.cin == 128)) {
+            else if (split && L.dil <= 4 && L.soff16 >= 0 && !NPD_CONV_WS16_OFF) {
+                // cin 32 / 64: 16x16x32 weight-stationary kernel, no channel parts; one 8-wave block per CU, a multiple of
+                // the 64-channel slice count; 128-position items where N allows
+                const int kbn = L.cin / 32;
+                const int Q = N % 128 == 0 ? 2 : 1;
+                const int nslices = (L.cout + 63) / 64;
+                const int64_t items = nb * (N / (64 * Q)) * nslices;
+                int64_t nblk = (int64_t)device_cu_count();
+                nblk -= nblk % nslices;
+                if (nblk > items) nblk = items;
+                if (nblk < nslices) nblk = nslices;
+                const size_t ls = ws16_lds_bytes(kbn, Q, L.dil);
+                const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff16);
+#define NPD_WS16(KBV, QV)                                                                                          \
+    hipLaunchKernelGGL((conv_ws16_kernel<KBV, QV>), dim3((unsigned)nblk), dim3(512), ls, s, in, o, rsrc, wi,         \
+                       c->img + L.boff, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
+                if (kbn == 2) { if (Q == 2) NPD_WS16(2, 2); else NPD_WS16(2, 1); }
+                else { if (Q == 2) NPD_WS16(1, 2); else NPD_WS16(1, 1); }
+#undef NPD_WS16
+            } else if (split && L.dil <= 4 && (L.cin <= 64 || L.cin == 128)) {
                 // weight-stationary persistent blocks: one per CU, a multiple of the 64-channel slice count.
                 // cin <= 48: 4 waves (KS 1); 64: 4 waves, 2 channel parts, two blocks per CU; 128: 8 waves, 4 channel
                 // parts, 64-position items (the 128-position slab would not fit).  Other widths (e.g. 80, 96: a 2-part
@@ -1218,9 +1749,62 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 uint32_t* am_out = f < 2 ? amax + (kLayers + f) * kAmaxWords : nullptr;  // FC2 feeds the fp32 LayerNorm
                 if (fo[f] % FB == 0) {
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    hipLaunchKernelGGL((fc_split_big_kernel<2, 2>), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,
-                                       c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
-                                       am_in, am_out);
+                    if (NPD_FC_WSP && fk[f] % 32 == 0) {
+                        const float* xa = fin[f];
+                        int lda = fk[f], ldb = fk[f];
+#if NPD_FC_PANELEXP
+                        // experiment: panel-major copies of X (per call) and of the weight planes (once)
+                        static float* xp = nullptr;
+                        static uint16_t* wp[3][2] = {};
+                        if (!xp) NPD_HIP(hipMalloc(&xp, (size_t)Bc * fk[0] * 4));
+                        if (!wp[f][0])
+                            for (int q = 0; q < 2; ++q) {
+                                NPD_HIP(hipMalloc(&wp[f][q], (size_t)fo[f] * fk[f] * 2));
+                                const int64_t n8 = (int64_t)fo[f] * fk[f] / 8;
+                                hipLaunchKernelGGL(panel16_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s,
+                                                   q ? wl : wh, wp[f][q], fo[f], fk[f]);
+                            }
+                        {
+                            const int64_t n4 = (int64_t)nb * fk[f] / 4;
+                            hipLaunchKernelGGL(panel32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, fin[f],
+                                               xp, (int)nb, fk[f]);
+                        }
+                        xa = xp;
+                        wh = wp[f][0];
+                        wl = wp[f][1];
+                        lda = 0;
+                        ldb = 0;
+#endif
+#if NPD_FC_PADEXP
+                        // experiment: row strides padded by NPD_FC_PADEXP elements (X copied, weight planes copied once)
+                        static float* xp = nullptr;
+                        static uint16_t* wp[3][2] = {};
+                        const int pad = NPD_FC_PADEXP;
+                        if (!xp) NPD_HIP(hipMalloc(&xp, (size_t)Bc * (fk[0] + pad) * 4));
+                        if (!wp[f][0])
+                            for (int q = 0; q < 2; ++q) {
+                                NPD_HIP(hipMalloc(&wp[f][q], (size_t)fo[f] * (fk[f] + pad) * 2));
+                                NPD_HIP(hipMemcpy2D(wp[f][q], (size_t)(fk[f] + pad) * 2, q ? wl : wh, (size_t)fk[f] * 2,
+                                                    (size_t)fk[f] * 2, fo[f], hipMemcpyDeviceToDevice));
+                            }
+                        NPD_HIP(hipMemcpy2DAsync(xp, (size_t)(fk[f] + pad) * 4, fin[f], (size_t)fk[f] * 4, (size_t)fk[f] * 4,
+                                                 nb, hipMemcpyDeviceToDevice, s));
+                        xa = xp;
+                        wh = wp[f][0];
+                        wl = wp[f][1];
+                        lda = fk[f] + pad;
+                        ldb = fk[f] + pad;
+#endif
+                        hipLaunchKernelGGL((FC_WSP), gb, dim3(512), kFcWspLds, s, xa, wh, wl, c->img + c->off_fc[f][1],
+                                           fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f], am_in, am_out, lda, ldb);
+                    }
+                    else if (fk[f] % NPD_FC_GK == 0)
+                        hipLaunchKernelGGL((FC_BIG), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl, c->img + c->off_fc[f][1],
+                                           fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f], am_in, am_out);
+                    else
+                        hipLaunchKernelGGL((FC_BIG_32), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,
+                                           c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
+                                           am_in, am_out);
                 } else {
                     hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
