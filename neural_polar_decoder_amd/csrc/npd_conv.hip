@@ -526,9 +526,6 @@ __device__ __forceinline__ f4 mfma16x32(const hf8& a, const hf8& b, const f4& c)
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-#ifndef NPD_WS_PROBE
-#define NPD_WS_PROBE 0  // timing probes only (wrong results): 1 no MFMAs, 2 no activation loads, 3 no slab stores
-#endif
 template <int KB, int Q>
 __global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                            const float* __restrict__ res, const f4* __restrict__ wimg,
@@ -580,7 +577,7 @@ __global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restri
             const int p = idx / C4P, c4 = idx - p * C4P;
             const int l = l0 - halo + p;
             f4 v = f4{0.f, 0.f, 0.f, 0.f};
-            if (NPD_WS_PROBE != 2 && p < W && l >= 0 && l < N) v = inb[(int64_t)l * C4P + c4];
+            if (p < W && l >= 0 && l < N) v = inb[(int64_t)l * C4P + c4];
             pre[e] = v;
         }
     };
@@ -597,10 +594,6 @@ __global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restri
                     const float x = pre[e][j] * sa_scale;
                     hi[j] = (_Float16)x;
                     lo[j] = (_Float16)(x - (float)hi[j]);
-                }
-                if (NPD_WS_PROBE == 3) {
-                    if ((float)hi[0] + (float)lo[3] == 12345.f) hiP[tid] = hi[1];
-                    continue;
                 }
                 *reinterpret_cast<hf4*>(hiP + p * CSH + 4 * c4) = hi;
                 *reinterpret_cast<hf4*>(hiP + plane + p * CSH + 4 * c4) = lo;
@@ -642,10 +635,6 @@ __global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restri
                     const int off = (tbase + 16 * q + dil * t) * CSH + 32 * kb + 8 * g;
                     const hf8 bh = *reinterpret_cast<const hf8*>(hiP + off);
                     const hf8 bl = *reinterpret_cast<const hf8*>(loP + off);
-                    if (NPD_WS_PROBE == 1) {
-                        acc[q][0] += (float)bh[t] + (float)bl[kb] + (float)ah[t][kb][q] + (float)al[t][kb][q + 1];
-                        continue;
-                    }
                     acc[q] = mfma16x32(ah[t][kb], bh, acc[q]);
                     acc[q] = mfma16x32(ah[t][kb], bl, acc[q]);
                     acc[q] = mfma16x32(al[t][kb], bh, acc[q]);
@@ -840,41 +829,19 @@ __global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
 
-// fp16x3 FC GEMM with a 128 x 128 block tile (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from N = 128), each
-// X / W element staged in LDS read by 4 MFMA tiles instead of the 64 x 64 kernel's 2.  WM x WN waves: 2 x 2 (64 x 64
-// per wave, 16 ds_read_b128 per 24 MFMAs of a 32-wide K block; used) or 2 x 4 (64 x 32 per wave, two waves per
-// SIMD): measured equal, 408 vs 414 us average over FC0-FC2 per 4096 codewords (profiles/round4/conv_kernel_stats*.csv).  At one workgroup per CU a K block's MFMAs (~770 SIMD cycles) are shorter than an HBM round trip, so the loads
-// run FD = 3 K blocks ahead through a register ring, split / stored into the other LDS buffer one block ahead.  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2): the column tiles of one row
-// block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords -- is read from HBM once, not once per
-// column tile.  LDS 144 KB (dynamic).
+// fp16x3 FC GEMM with a 128 x 128 block tile (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from N = 128; K is
+// E N, 4 N or N, always a multiple of 32).  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2):
+// the column tiles of one row block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords at configs[4]
+// -- comes from HBM about once (PMC: 1.8-2.1 GB fetched per FC0 launch against 0.54 GB of X and 8 x 0.13 GB of
+// weight planes, one copy per XCD).  What bounds it (round 5 timing probes, FC0 ~1.0-1.2 ms per 4096 codewords): the
+// operand stream into each CU.  Every K block moves 32 KB (X 16 KB fp32, W 2 x 8 KB fp16) into a CU for 24 MFMAs per
+// wave; with the loads replaced by constants the same kernel ran 0.62 ms, with the MFMAs removed 0.8 ms; deeper
+// register rings (3-6 K blocks), padded row strides and panel-major copies of both operands (16 KB contiguous per K
+// block) all measured within 2 %: ~32 GB/s per CU of mixed L2 / HBM reads, the per-CU load rate MI355X_MICROARCH.md
+// measures for such streams (23-73 GB/s).  Fewer bytes per MFMA need a bigger tile (256 x 128 or 256 x 256), which
+// needs 8192 or 16384 codewords per chunk to fill 256 CUs.
 constexpr int FB = 128;
 
-// LDS row stride of the 128-row planes: 72 halfs (144 B = 36 banks, as the conv slabs) -- the 64 x 64 kernel's 40
-// (80 B = 20 banks) left a third of this kernel's LDS cycles bank-conflicted (PMC SQ_LDS_BANK_CONFLICT /
-// SQ_LDS_IDX_ACTIVE, profiles/round4/pmc_conv_summary.json); removing them moved the kernel by 2 % (405 vs 408-414 us
-// average per 4096 codewords, conv_kernel_stats_v4.csv): the conflicts were not its limit
-constexpr int GSB = 72;
-constexpr size_t kFcBigLds = (size_t)2 * 4 * FB * GSB * 2;
-
-// WM x WN waves over the 128 x 128 tile, each (128 / WM) x (128 / WN) = TM x TN MFMA tiles of 32 x 32.  K blocks of
-// GKT (32 or 64) run through an FDT-deep register ring; a step is ONE basic block (the ring's prefetch index is clamped
-// at the tail instead of branched on, the last step's spare stash lands in the buffer nobody reads any more), and the
-// split / store of block kb + 1 is cut into GKT / 16 parts issued beside the MFMAs of block kb's k-steps, whose
-// fragments are read one k-step ahead -- so the compiler can fill the MFMA gaps with the split and the LDS stores
-// instead of running them after the MFMAs, at one wave per SIMD.  The activation scale's amax words are loaded before
-// the first K blocks and reduced after them.
-#ifndef NPD_FC_GK
-#define NPD_FC_GK 32
-#endif
-#ifndef NPD_FC_FD
-#define NPD_FC_FD 3
-#endif
-#ifndef NPD_FC_PROBE
-#define NPD_FC_PROBE 0  // timing probes only (wrong results): 1 no MFMAs, 2 no loads, 3 no LDS stores
-#endif
-#ifndef NPD_FC_SG
-#define NPD_FC_SG 0
-#endif
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (I < N) {
@@ -883,221 +850,14 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <int WM, int WN, int GKT, int FDT>
-__global__ __launch_bounds__(64 * WM * WN) void fc_split_big_kernel(const float* __restrict__ X,
-                                                                    const uint16_t* __restrict__ Whi,
-                                                                    const uint16_t* __restrict__ Wlo,
-                                                                    const float* __restrict__ bias,
-                                                                    float* __restrict__ out, int M, int K, int Nout,
-                                                                    int act, int sw, const uint32_t* __restrict__ amax_in,
-                                                                    uint32_t* __restrict__ amax_out) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int TM = FB / 32 / WM, TN = FB / 32 / WN;
-    constexpr int ST = GKT / 16;                                 // k-steps per K block
-    constexpr int A4 = GKT / 4, B8 = GKT / 8;                    // f4 per A row, 16-B pieces per B row
-    constexpr int UA = FB * A4 / NT, UB = FB * B8 / NT;          // per thread: A f4 loads, B loads per plane
-    constexpr int PA = UA / ST, PB = UB / ST;                    // per stash part
-    static_assert(UA % ST == 0 && UB % ST == 0 && GKT + 8 <= GSB, "FC tile");
-    const uint32_t am_raw = amax_in != nullptr ? __builtin_nontemporal_load(amax_in + (threadIdx.x & 63) * kAmaxStride) : 0u;
-    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [buf][plane A hi, A lo, B hi, B lo][128][GSB]
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int h = lane >> 5, col = lane & 31;
-    // XCD-aware tile order (grid = column tiles x row tiles, a multiple of 8 or dealt linearly)
-    const int gx = Nout / FB;
-    const int total = gridDim.x;
-    int lin = blockIdx.x;
-    if ((total & 7) == 0) lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-    const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
-    const int wm = wave % WM, wn = wave / WM;
-    constexpr int PL = FB * GSB;  // halfs per plane
-    f4 ra[FDT][UA], rbh[FDT][UB], rbl[FDT][UB];
-    auto fetch = [&](int slot, int k0) {
-        if (NPD_FC_PROBE == 2) {
-#pragma unroll
-            for (int u = 0; u < UA; ++u) ra[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
-#pragma unroll
-            for (int u = 0; u < UB; ++u) rbh[slot][u] = rbl[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
-            return;
-        }
-#pragma unroll
-        for (int u = 0; u < UA; ++u) {
-            const int idx = tid + NT * u;
-            const int r = idx / A4, c4 = (idx % A4) * 4;
-            int mr = m0 + r;
-            if (mr >= M) mr = M - 1;
-            ra[slot][u] = *reinterpret_cast<const f4*>(X + (int64_t)mr * K + k0 + c4);
-        }
-#pragma unroll
-        for (int u = 0; u < UB; ++u) {
-            const int idx = tid + NT * u;
-            const int r = idx / B8, c8 = (idx % B8) * 8;
-            rbh[slot][u] = *reinterpret_cast<const f4*>(Whi + (int64_t)(j0 + r) * K + k0 + c8);
-            rbl[slot][u] = *reinterpret_cast<const f4*>(Wlo + (int64_t)(j0 + r) * K + k0 + c8);
-        }
-    };
-    float sa_scale = 1.0f;
-    auto stash = [&](int slot, int buf, int part) {
-        _Float16* const base = smb + (size_t)buf * 4 * PL;
-        if (NPD_FC_PROBE == 3) {
-            float q = 0.f;
-#pragma unroll
-            for (int v = 0; v < PA; ++v) q += ra[slot][part * PA + v][0] + ra[slot][part * PA + v][3];
-#pragma unroll
-            for (int v = 0; v < PB; ++v) q += rbh[slot][part * PB + v][0] + rbl[slot][part * PB + v][1];
-            if (q == 12345.f) base[tid] = (_Float16)q;
-            return;
-        }
-#pragma unroll
-        for (int v = 0; v < PA; ++v) {
-            const int u = part * PA + v;
-            const int idx = tid + NT * u;
-            const int r = idx / A4, c4 = (idx % A4) * 4;
-            hf4 hi, lo;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float x = ra[slot][u][e] * sa_scale;
-                hi[e] = (_Float16)x;
-                lo[e] = (_Float16)(x - (float)hi[e]);
-            }
-            *reinterpret_cast<hf4*>(base + r * GSB + c4) = hi;
-            *reinterpret_cast<hf4*>(base + PL + r * GSB + c4) = lo;
-        }
-#pragma unroll
-        for (int v = 0; v < PB; ++v) {
-            const int u = part * PB + v;
-            const int idx = tid + NT * u;
-            const int r = idx / B8, c8 = (idx % B8) * 8;
-            *reinterpret_cast<f4*>(base + 2 * PL + r * GSB + c8) = rbh[slot][u];
-            *reinterpret_cast<f4*>(base + 3 * PL + r * GSB + c8) = rbl[slot][u];
-        }
-    };
-    f16v acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-            acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const int nk = K / GKT;
-    const int ar = (wm * 32 * TM + col) * GSB + 8 * h, br = (wn * 32 * TN + col) * GSB + 8 * h;
-    // K block kb lives in ring slot kb % FDT until it is stashed into LDS buffer kb & 1
-#pragma unroll
-    for (int d = 0; d < FDT; ++d) fetch(d, min(d, nk - 1) * GKT);
-    const int sa = amax_in != nullptr ? min(kSplitSA, 15 - ((int)((wave_max_u32(am_raw) >> 23) & 0xFFu) - 126)) : kSplitSA;
-    sa_scale = __builtin_ldexpf(1.0f, sa);
-    const float descale = __builtin_ldexpf(1.0f, -(sw + sa));
-#pragma unroll
-    for (int p = 0; p < ST; ++p) stash(0, 0, p);
-    __syncthreads();
-    struct Frags {
-        hf8 ah[TM], al[TM], bh[TN], bl[TN];
-    };
-    auto read = [&](const _Float16* cb, int st, Frags& f) {
-#pragma unroll
-        for (int t = 0; t < TM; ++t) {
-            f.ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GSB + 16 * st);
-            f.al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GSB + 16 * st);
-        }
-#pragma unroll
-        for (int t = 0; t < TN; ++t) {
-            f.bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GSB + 16 * st);
-            f.bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GSB + 16 * st);
-        }
-    };
-    auto step = [&](int kb, auto slot_c) {
-        constexpr int SL = decltype(slot_c)::value;  // kb % FDT
-        const _Float16* const cb = smb + (size_t)(kb & 1) * 4 * PL;
-        fetch(SL, min(kb + FDT, nk - 1) * GKT);  // slot SL was stashed at step kb - 1
-        Frags f[2];
-        read(cb, 0, f[0]);
-#pragma unroll
-        for (int st = 0; st < ST; ++st) {
-            if (st + 1 < ST) read(cb, st + 1, f[(st + 1) & 1]);
-            const Frags& c = f[st & 1];
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b) {
-                    if (NPD_FC_PROBE == 1) {
-                        acc[a][b][0] += (float)c.ah[a][0] + (float)c.bh[b][1] + (float)c.al[a][2] + (float)c.bl[b][3];
-                        continue;
-                    }
-                    acc[a][b] = mfma16(c.ah[a], c.bh[b], acc[a][b]);
-                    acc[a][b] = mfma16(c.ah[a], c.bl[b], acc[a][b]);
-                    acc[a][b] = mfma16(c.al[a], c.bh[b], acc[a][b]);
-                }
-            stash((SL + 1) % FDT, (kb + 1) & 1, st);
-#if NPD_FC_SG
-#pragma unroll
-            for (int i = 0; i < TM * TN * 3; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                if (i % 3 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-            }
-#endif
-        }
-        __syncthreads();
-    };
-    int kb = 0;
-    for (; kb + FDT <= nk; kb += FDT) static_for<0, FDT>([&](auto i) { step(kb + i.value, i); });
-    static_for<0, FDT>([&](auto i) {
-        if (kb + i.value < nk) step(kb + i.value, i);
-    });
-    float amx = 0.0f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int j = j0 + wn * 32 * TN + 32 * b + col;
-            const float bj = bias[j];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * 32 * TM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M) {
-                    float v = fmaf(acc[a][b][r], descale, bj);
-                    if (act) v = gelu(v);
-                    out[(int64_t)m * Nout + j] = v;
-                    amx = fmaxf(amx, fabsf(v));
-                }
-            }
-        }
-    if (amax_out != nullptr) publish_amax(amax_out, amx);
-}
-#define FC_BIG fc_split_big_kernel<2, 2, NPD_FC_GK, NPD_FC_FD>
-#define FC_BIG_32 fc_split_big_kernel<2, 2, 32, 3>
-
-// The same 128 x 128 fp16x3 tile with the waves specialised (512 threads, two waves per SIMD): waves 0-3 only read
-// fragments and issue MFMAs (64 x 64 each, as above); waves 4-7 only load, split and store.  The loaders keep FDL K
-// blocks in flight in their registers and fill an NS-slot LDS ring two blocks ahead of the MFMA waves; one barrier per
-// K block.  With one wave per SIMD the split, the LDS stores and the waits for HBM sat between a SIMD's MFMAs
-// (fc_split_big_kernel's MFMA-free timing probe ran 94 % as long as the kernel); here they run on the SIMD's other wave.
-#ifndef NPD_FC_WSP
-#define NPD_FC_WSP 1
-#endif
+// The waves are specialised (512 threads, two waves per SIMD): waves 0-3 only read fragments and issue MFMAs (64 x 64
+// each, v_mfma_f32_32x32x16_f16, three per product); waves 4-7 only load, split (x 2^SA) and store.  The loaders keep
+// FDL K blocks in flight in their registers and fill a 3-slot LDS ring two blocks ahead of the MFMA waves, which read
+// the next block's first fragments during the current block's MFMAs; one LDS-only barrier per K block.  Against the
+// round-4 kernel (4 waves each loading and computing, one per SIMD): 355-365 vs 386-412 us average over FC0-FC2.
 #ifndef NPD_FC_FDL
 #define NPD_FC_FDL 3
 #endif
-#ifndef NPD_FC_PADEXP
-#define NPD_FC_PADEXP 0
-#endif
-#ifndef NPD_FC_PANELEXP
-#define NPD_FC_PANELEXP 0
-#endif
-// (rows, K) row-major -> [K / 32][rows][32] panels (experiment copies)
-__global__ void panel32_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int K) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)rows * K / 4) return;
-    const int64_t m = i / (K / 4);
-    const int k = (int)(i % (K / 4)) * 4;
-    *reinterpret_cast<f4*>(dst + ((int64_t)(k / 32) * rows + m) * 32 + k % 32) = *reinterpret_cast<const f4*>(src + m * K + k);
-}
-__global__ void panel16_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, int rows, int K) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)rows * K / 8) return;
-    const int64_t m = i / (K / 8);
-    const int k = (int)(i % (K / 8)) * 8;
-    *reinterpret_cast<f4*>(dst + ((int64_t)(k / 32) * rows + m) * 32 + k % 32) = *reinterpret_cast<const f4*>(src + m * K + k);
-}
 // workgroup barrier that orders LDS only: a __syncthreads() also waits for every global load in flight (vmcnt(0)),
 // which would drain the loaders' register ring at each K block
 __device__ __forceinline__ void lds_barrier() {
@@ -1114,7 +874,7 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
                                                               const float* __restrict__ bias, float* __restrict__ out,
                                                               int M, int K, int Nout, int act, int sw,
                                                               const uint32_t* __restrict__ amax_in,
-                                                              uint32_t* __restrict__ amax_out, int lda, int ldb) {
+                                                              uint32_t* __restrict__ amax_out) {
     constexpr int GKT = 32, NS = kWspSlots;
     static_assert(FDL >= 2 && FDL % NS == 0, "the prologue stashes two K blocks; LDS slots repeat with the ring");
     constexpr int NL = 256;                            // loader threads
@@ -1146,30 +906,22 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
             const int idx = lt + NL * u;
             const int r = idx / A4, c4 = (idx % A4) * 4;
             const int mr = min(m0 + r, M - 1);
-            offA[u] = (uint32_t)((lda ? (int64_t)mr * lda + c4 : (int64_t)mr * GKT + c4) * 4);
+            offA[u] = (uint32_t)(((int64_t)mr * K + c4) * 4);
             ldsA[u] = (uint32_t)(r * GSW + c4);
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const int idx = lt + NL * u;
             const int r = idx / B8, c8 = (idx % B8) * 8;
-            offB[u] = (uint32_t)((ldb ? (int64_t)(j0 + r) * ldb + c8 : (int64_t)(j0 + r) * GKT + c8) * 2);
+            offB[u] = (uint32_t)(((int64_t)(j0 + r) * K + c8) * 2);
             ldsB[u] = (uint32_t)(r * GSW + c8);
         }
         f4 ra[FDL][UA], rbh[FDL][UB], rbl[FDL][UB];
         auto fetch = [&](int slot, int kb) {
             const int k0 = min(kb, nk - 1) * GKT;
-            if (NPD_FC_PROBE == 2) {
-#pragma unroll
-                for (int u = 0; u < UA; ++u) ra[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
-#pragma unroll
-                for (int u = 0; u < UB; ++u) rbh[slot][u] = rbl[slot][u] = f4{(float)k0, 1.f, 2.f, 3.f};
-                return;
-            }
-            // lda / ldb 0: panel-major operand, [K / 32][rows][32]
-            const char* const xk = reinterpret_cast<const char*>(X) + (lda ? (size_t)k0 : (size_t)k0 * M) * 4;
-            const char* const hk = reinterpret_cast<const char*>(Whi) + (ldb ? (size_t)k0 : (size_t)k0 * Nout) * 2;
-            const char* const lk = reinterpret_cast<const char*>(Wlo) + (ldb ? (size_t)k0 : (size_t)k0 * Nout) * 2;
+            const char* const xk = reinterpret_cast<const char*>(X) + (size_t)k0 * 4;
+            const char* const hk = reinterpret_cast<const char*>(Whi) + (size_t)k0 * 2;
+            const char* const lk = reinterpret_cast<const char*>(Wlo) + (size_t)k0 * 2;
 #pragma unroll
             for (int u = 0; u < UA; ++u) ra[slot][u] = *reinterpret_cast<const f4*>(xk + offA[u]);
 #pragma unroll
@@ -1266,10 +1018,6 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
                 for (int a = 0; a < TM; ++a)
 #pragma unroll
                     for (int b = 0; b < TN; ++b) {
-                        if (NPD_FC_PROBE == 1) {
-                            acc[a][b][0] += (float)c.ah[a][0] + (float)c.bh[b][1] + (float)c.al[a][2] + (float)c.bl[b][3];
-                            continue;
-                        }
                         acc[a][b] = mfma16(c.ah[a], c.bh[b], acc[a][b]);
                         acc[a][b] = mfma16(c.ah[a], c.bl[b], acc[a][b]);
                         acc[a][b] = mfma16(c.al[a], c.bh[b], acc[a][b]);
@@ -1614,8 +1362,6 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_BIG, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcBigLds));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_BIG_32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcBigLds));
         NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
         const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
@@ -1749,62 +1495,8 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 uint32_t* am_out = f < 2 ? amax + (kLayers + f) * kAmaxWords : nullptr;  // FC2 feeds the fp32 LayerNorm
                 if (fo[f] % FB == 0) {
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    if (NPD_FC_WSP && fk[f] % 32 == 0) {
-                        const float* xa = fin[f];
-                        int lda = fk[f], ldb = fk[f];
-#if NPD_FC_PANELEXP
-                        // experiment: panel-major copies of X (per call) and of the weight planes (once)
-                        static float* xp = nullptr;
-                        static uint16_t* wp[3][2] = {};
-                        if (!xp) NPD_HIP(hipMalloc(&xp, (size_t)Bc * fk[0] * 4));
-                        if (!wp[f][0])
-                            for (int q = 0; q < 2; ++q) {
-                                NPD_HIP(hipMalloc(&wp[f][q], (size_t)fo[f] * fk[f] * 2));
-                                const int64_t n8 = (int64_t)fo[f] * fk[f] / 8;
-                                hipLaunchKernelGGL(panel16_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s,
-                                                   q ? wl : wh, wp[f][q], fo[f], fk[f]);
-                            }
-                        {
-                            const int64_t n4 = (int64_t)nb * fk[f] / 4;
-                            hipLaunchKernelGGL(panel32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, fin[f],
-                                               xp, (int)nb, fk[f]);
-                        }
-                        xa = xp;
-                        wh = wp[f][0];
-                        wl = wp[f][1];
-                        lda = 0;
-                        ldb = 0;
-#endif
-#if NPD_FC_PADEXP
-                        // experiment: row strides padded by NPD_FC_PADEXP elements (X copied, weight planes copied once)
-                        static float* xp = nullptr;
-                        static uint16_t* wp[3][2] = {};
-                        const int pad = NPD_FC_PADEXP;
-                        if (!xp) NPD_HIP(hipMalloc(&xp, (size_t)Bc * (fk[0] + pad) * 4));
-                        if (!wp[f][0])
-                            for (int q = 0; q < 2; ++q) {
-                                NPD_HIP(hipMalloc(&wp[f][q], (size_t)fo[f] * (fk[f] + pad) * 2));
-                                NPD_HIP(hipMemcpy2D(wp[f][q], (size_t)(fk[f] + pad) * 2, q ? wl : wh, (size_t)fk[f] * 2,
-                                                    (size_t)fk[f] * 2, fo[f], hipMemcpyDeviceToDevice));
-                            }
-                        NPD_HIP(hipMemcpy2DAsync(xp, (size_t)(fk[f] + pad) * 4, fin[f], (size_t)fk[f] * 4, (size_t)fk[f] * 4,
-                                                 nb, hipMemcpyDeviceToDevice, s));
-                        xa = xp;
-                        wh = wp[f][0];
-                        wl = wp[f][1];
-                        lda = fk[f] + pad;
-                        ldb = fk[f] + pad;
-#endif
-                        hipLaunchKernelGGL((FC_WSP), gb, dim3(512), kFcWspLds, s, xa, wh, wl, c->img + c->off_fc[f][1],
-                                           fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f], am_in, am_out, lda, ldb);
-                    }
-                    else if (fk[f] % NPD_FC_GK == 0)
-                        hipLaunchKernelGGL((FC_BIG), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl, c->img + c->off_fc[f][1],
-                                           fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f], am_in, am_out);
-                    else
-                        hipLaunchKernelGGL((FC_BIG_32), gb, dim3(256), kFcBigLds, s, fin[f], wh, wl,
-                                           c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
-                                           am_in, am_out);
+                    hipLaunchKernelGGL((FC_WSP), gb, dim3(512), kFcWspLds, s, fin[f], wh, wl, c->img + c->off_fc[f][1],
+                                       fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f], am_in, am_out);
                 } else {
                     hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
