@@ -618,7 +618,7 @@ def conv_leg(dev, rank, world, timer, batch=8192):
             "dtype": "fp16x3: conv layers (cin > 1) and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo fp16 split, "
                      "3 products, fp32 accumulation; layer 0, epilogues and LayerNorm fp32",
             "achieved_tflops_fp32_equivalent": p16["tf"],
-            "roofline": {"bound": "mfma", "kernel": "conv_split_ws_kernel / fc_split_big_kernel (fp16x3)",
+            "roofline": {"bound": "mfma", "kernel": "conv_ws16_kernel / conv_split_ws_kernel / fc_split_wsp_kernel (fp16x3)",
                          "achieved": 3 * p16["tf"], "unit": "TFLOP/s (fp16 MFMA work issued: 3 products)",
                          "peak": FP16_PEAK_TF, "frac": 3 * p16["tf"] / FP16_PEAK_TF},
             "max_abs_logit_diff_vs_fp32": float((p16["lg"] - p32["lg"]).abs().max()),

@@ -9,7 +9,7 @@ Implementations:
   * "reference" -- the reference's arithmetic (models.py:742-767: Conv1d + GELU blocks, residuals, flatten c*N + l,
                    Linear + GELU, Linear + GELU, Linear, LayerNorm(eps 1e-6)) as torch fp32 ops on the CPU;
   * "fp32"      -- the HIP fp32 path the bench times (conv_layer_kernel / fc_kernel, v_mfma_f32_32x32x2_f32);
-  * "fp16x3"    -- the split path (conv_split_ws_kernel / fc_split_big_kernel, hi + lo fp16, three products).
+  * "fp16x3"    -- the split path (conv_ws16_kernel / conv_split_ws_kernel / fc_split_wsp_kernel, hi + lo fp16, three products).
 Decision flips are counted against the float64 decisions (sign of the logit)."""
 import argparse
 import json
