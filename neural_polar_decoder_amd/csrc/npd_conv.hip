@@ -50,9 +50,6 @@ struct LayerDesc {
 // (split_sa: max |a| 2^SA < 2^15, so hi cannot overflow fp16); the weights of each layer are scaled by 2^SW on the host
 // so that max |w| 2^SW is in [2^12, 2^13) (hi and lo normal for |w| >= max |w| 2^-11)
 constexpr int kSplitSA = 4;
-#ifndef NPD_CONV_WS16_OFF
-#define NPD_CONV_WS16_OFF 0
-#endif
 
 
 
@@ -1399,7 +1396,7 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             if (L.cin == 1)
                 hipLaunchKernelGGL(conv_layer_kernel<true>, grid, dim3(256), lds, s, in, o, rsrc, c->img + L.woff,
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, am_out);
-            else if (split && L.dil <= 4 && L.soff16 >= 0 && !NPD_CONV_WS16_OFF) {
+            else if (split && L.dil <= 4 && L.soff16 >= 0) {
                 // cin 32 / 64: 16x16x32 weight-stationary kernel, no channel parts; one 8-wave block per CU, a multiple of
                 // the 64-channel slice count; 128-position items where N allows
                 const int kbn = L.cin / 32;
