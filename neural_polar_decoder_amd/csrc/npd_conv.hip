@@ -523,20 +523,37 @@ __device__ __forceinline__ f4 mfma16x32(const hf8& a, const hf8& b, const f4& c)
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-template <int KB, int Q>
-__global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restrict__ in, float* __restrict__ out,
+// A/B switches: waves per block (8: one block per CU; 4: two) and 128-position items where N allows (1) -- measured
+// 234 us (8, 1) / 245 us (4, 0) / 253 us (8, 1, CIN + 8 rows) per 64-channel layer per 4096 codewords
+#ifndef NPD_WS16_NW
+#define NPD_WS16_NW 8
+#endif
+#ifndef NPD_WS16_Q2
+#define NPD_WS16_Q2 1
+#endif
+#ifndef NPD_WS16_PAD
+#define NPD_WS16_PAD 16
+#endif
+template <int KB, int Q, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                            const float* __restrict__ res, const f4* __restrict__ wimg,
                                                            const float* __restrict__ bias, int cout, int N, int dil,
                                                            int do_res, int sw, const uint32_t* __restrict__ amax_in,
                                                            uint32_t* __restrict__ amax_out, int64_t nb, int nslices) {
     extern __shared__ __attribute__((aligned(16))) _Float16 slab16[];
-    constexpr int NT = 512;
+    constexpr int NT = 64 * NW;
     constexpr int CIN = 32 * KB;
     constexpr int PT = 64 * Q;        // positions per item
     constexpr int C4P = CIN / 4;      // float4 channel groups per staged row
-    constexpr int CSH = CIN + 8;      // fp16 row stride of the LDS slab (conflict-free ds_read_b128)
+    // fp16 row stride of the LDS slab: CIN + 16 halfs.  A B fragment read (lane 16 g + c: row c, channels 8 g ..) puts
+    // rows c at c * CSH / 8 16-B units and g at +g units; with CIN + 8 (36 / 20 dwords) ds_read_b128's lane groups
+    // {0-3, 12-15, 20-27}, ... collided 2-way (PMC: SQ_LDS_BANK_CONFLICT 0.48 of SQ_LDS_IDX_ACTIVE), with CIN + 16
+    // (40 / 24 dwords) every group hits 16 distinct units
+    constexpr int CSH = CIN + NPD_WS16_PAD;
     constexpr int MAXE = ((PT + 24) * C4P + NT - 1) / NT;
-    constexpr int TPW = 2 * Q;        // 16-position tiles per wave
+    constexpr int PP = NW / 4;        // position parts
+    constexpr int TPW = 4 * Q / PP;   // 16-position tiles per wave
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, col = lane & 15;
@@ -655,7 +672,7 @@ __global__ __launch_bounds__(512, 1) void conv_ws16_kernel(const float* __restri
 }
 
 static size_t ws16_lds_bytes(int kb, int Q, int dil) {
-    return (size_t)2 * 2 * (64 * Q + 6 * dil) * (32 * kb + 8) * 2;
+    return (size_t)2 * 2 * (64 * Q + 6 * dil) * (32 * kb + NPD_WS16_PAD) * 2;
 }
 
 // ------------------------------------------------------------------------------ FC GEMM
@@ -1365,8 +1382,8 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<4, 1, 2, 4>, (const void*)conv_split_ws_kernel<8, 1, 4, 8>};
         for (const void* k : ws) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
-        const void* w16[4] = {(const void*)conv_ws16_kernel<1, 1>, (const void*)conv_ws16_kernel<1, 2>,
-                              (const void*)conv_ws16_kernel<2, 1>, (const void*)conv_ws16_kernel<2, 2>};
+        const void* w16[4] = {(const void*)conv_ws16_kernel<1, 1, NPD_WS16_NW>, (const void*)conv_ws16_kernel<1, 2, NPD_WS16_NW>,
+                              (const void*)conv_ws16_kernel<2, 1, NPD_WS16_NW>, (const void*)conv_ws16_kernel<2, 2, NPD_WS16_NW>};
         for (const void* k : w16) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
     }
@@ -1400,18 +1417,18 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 // cin 32 / 64: 16x16x32 weight-stationary kernel, no channel parts; one 8-wave block per CU, a multiple of
                 // the 64-channel slice count; 128-position items where N allows
                 const int kbn = L.cin / 32;
-                const int Q = N % 128 == 0 ? 2 : 1;
+                const int Q = N % 128 == 0 && NPD_WS16_Q2 ? 2 : 1;
                 const int nslices = (L.cout + 63) / 64;
                 const int64_t items = nb * (N / (64 * Q)) * nslices;
-                int64_t nblk = (int64_t)device_cu_count();
+                int64_t nblk = (int64_t)device_cu_count() * (8 / NPD_WS16_NW);
                 nblk -= nblk % nslices;
                 if (nblk > items) nblk = items;
                 if (nblk < nslices) nblk = nslices;
                 const size_t ls = ws16_lds_bytes(kbn, Q, L.dil);
                 const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff16);
 #define NPD_WS16(KBV, QV)                                                                                          \
-    hipLaunchKernelGGL((conv_ws16_kernel<KBV, QV>), dim3((unsigned)nblk), dim3(512), ls, s, in, o, rsrc, wi,         \
-                       c->img + L.boff, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
+    hipLaunchKernelGGL((conv_ws16_kernel<KBV, QV, NPD_WS16_NW>), dim3((unsigned)nblk), dim3(64 * NPD_WS16_NW), ls, s, \
+                       in, o, rsrc, wi, c->img + L.boff, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
                 if (kbn == 2) { if (Q == 2) NPD_WS16(2, 2); else NPD_WS16(2, 1); }
                 else { if (Q == 2) NPD_WS16(1, 2); else NPD_WS16(1, 1); }
 #undef NPD_WS16
