@@ -534,7 +534,10 @@ __device__ __forceinline__ f4 mfma16x32(const hf8& a, const hf8& b, const f4& c)
 #ifndef NPD_WS16_PAD
 #define NPD_WS16_PAD 16
 #endif
-template <int KB, int Q, int NW>
+#ifndef NPD_WS16_128
+#define NPD_WS16_128 1  // the 128-channel layer on conv_ws16_kernel<4, 1, 8, 2> (0: conv_split_ws_kernel<8, 1, 4, 8>)
+#endif
+template <int KB, int Q, int NW, int KP>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                            const float* __restrict__ res, const f4* __restrict__ wimg,
                                                            const float* __restrict__ bias, int cout, int N, int dil,
@@ -551,13 +554,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float*
     // (40 / 24 dwords) every group hits 16 distinct units
     constexpr int CSH = CIN + NPD_WS16_PAD;
     constexpr int MAXE = ((PT + 24) * C4P + NT - 1) / NT;
-    constexpr int PP = NW / 4;        // position parts
+    constexpr int PP = NW / 4 / KP;   // position parts
     constexpr int TPW = 4 * Q / PP;   // 16-position tiles per wave
-    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    constexpr int KBW = KB / KP;      // K blocks (32 input channels) per wave
+    static_assert((NW == 4 || NW == 8) && PP >= 1 && KB % KP == 0 && TPW % KP == 0, "wave decomposition");
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, col = lane & 15;
-    const int co16 = wave & 3, pp = wave >> 2;
+    const int co16 = wave & 3, kp = (wave >> 2) % KP, pp = (wave >> 2) / KP;
     const int halo = 3 * dil;
     const int W = PT + 2 * halo;
     const int plane = W * CSH;
@@ -565,17 +569,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float*
     const int t16 = slice * 4 + co16;  // 16-channel output tile
     const int sa = split_sa(amax_in);
     const float sa_scale = __builtin_ldexpf(1.0f, sa), descale = __builtin_ldexpf(1.0f, -(sw + sa));
-    hf8 ah[7][KB], al[7][KB];
+    hf8 ah[7][KBW], al[7][KBW];
     {
         const f4* wq = wimg + (int64_t)t16 * 7 * KB * 128 + lane;
 #pragma unroll
         for (int t = 0; t < 7; ++t)
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
-                ah[t][kb] = __builtin_bit_cast(hf8, wq[(t * KB + kb) * 128]);
-                al[t][kb] = __builtin_bit_cast(hf8, wq[(t * KB + kb) * 128 + 64]);
+            for (int kb = 0; kb < KBW; ++kb) {
+                ah[t][kb] = __builtin_bit_cast(hf8, wq[(t * KB + kp * KBW + kb) * 128]);
+                al[t][kb] = __builtin_bit_cast(hf8, wq[(t * KB + kp * KBW + kb) * 128 + 64]);
             }
     }
+    // KP = 2: the two channel parts of a 16-channel tile each finish half of its TPW position tiles, taking the other
+    // part's partial sums (one 16-B accumulator per lane and tile) from LDS behind the slab
+    f4* const red = reinterpret_cast<f4*>(slab16 + (size_t)4 * (PT + 24) * CSH);
+    auto fin = [&](int q) { return q * KP / TPW == kp; };
     const int chunks = N / PT;
     const int items = (int)nb * chunks;
     const int stride = gridDim.x / nslices;
@@ -633,7 +641,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float*
         f4 resv[TPW];
         if (do_res && co_ok) {
 #pragma unroll
-            for (int q = 0; q < TPW; ++q) resv[q] = *reinterpret_cast<const f4*>(res + (row0 + 16 * q) * cout + co);
+            for (int q = 0; q < TPW; ++q)
+                if (fin(q)) resv[q] = *reinterpret_cast<const f4*>(res + (row0 + 16 * q) * cout + co);
         }
         const _Float16* const hiP = slab16 + (size_t)buf * 2 * plane;
         const _Float16* const loP = hiP + plane;
@@ -643,19 +652,32 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float*
 #pragma unroll
         for (int t = 0; t < 7; ++t)
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb)
+            for (int kb = 0; kb < KBW; ++kb)
 #pragma unroll
                 for (int q = 0; q < TPW; ++q) {
-                    const int off = (tbase + 16 * q + dil * t) * CSH + 32 * kb + 8 * g;
+                    const int off = (tbase + 16 * q + dil * t) * CSH + 32 * (kp * KBW + kb) + 8 * g;
                     const hf8 bh = *reinterpret_cast<const hf8*>(hiP + off);
                     const hf8 bl = *reinterpret_cast<const hf8*>(loP + off);
                     acc[q] = mfma16x32(ah[t][kb], bh, acc[q]);
                     acc[q] = mfma16x32(ah[t][kb], bl, acc[q]);
                     acc[q] = mfma16x32(al[t][kb], bh, acc[q]);
                 }
+        if constexpr (KP > 1) {
+            const int slot = (co16 * PP + pp) * KP;
+#pragma unroll
+            for (int q = 0; q < TPW; ++q)
+                if (!fin(q)) red[((slot + kp) * TPW + q) * 64 + lane] = acc[q];
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < TPW; ++q)
+                if (fin(q))
+#pragma unroll
+                    for (int o = 1; o < KP; ++o) acc[q] += red[((slot + (kp + o) % KP) * TPW + q) * 64 + lane];
+        }
         if (co_ok) {
 #pragma unroll
             for (int q = 0; q < TPW; ++q) {
+                if (!fin(q)) continue;
                 f4 v;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = gelu(fmaf(acc[q][e], descale, bb[e]));
@@ -671,8 +693,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_ws16_kernel(const float*
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
 
-static size_t ws16_lds_bytes(int kb, int Q, int dil) {
-    return (size_t)2 * 2 * (64 * Q + 6 * dil) * (32 * kb + NPD_WS16_PAD) * 2;
+// slab: 2 buffers x (hi, lo) x (64 Q + 6 dil) rows; KP = 2: + the partial sums, 8 waves x TPW tiles x 64 lanes x 16 B
+// (the kernel places them after the dil = 4 slab)
+static size_t ws16_lds_bytes(int kb, int Q, int dil, int kp) {
+    const size_t slab = (size_t)2 * 2 * (64 * Q + 6 * (kp > 1 ? 4 : dil)) * (32 * kb + NPD_WS16_PAD) * 2;
+    return slab + (kp > 1 ? (size_t)8 * (2 * Q * kp) * 64 * 16 : 0);
 }
 
 // ------------------------------------------------------------------------------ FC GEMM
@@ -1211,7 +1236,7 @@ extern "C" int npd_conv_create(int N, int embed, const float* weights, int64_t n
                                 memcpy(&u16[e + 64 * 8], &lo, 2);
                             }
             L.soff16 = -1;
-            if (ci == 32 || ci == 64) {
+            if (ci == 32 || ci == 64 || (ci == 128 && NPD_WS16_128)) {
                 // conv_ws16_kernel A fragments [t16][tap][kb][part hi/lo][lane][8 x fp16]: 16x16x32 map, lane l = 16 g + r,
                 // element j = W[row 16 t16 + r][32 kb + 8 g + j][t] x 2^SW
                 const int kbn = ci / 32;
@@ -1382,8 +1407,10 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<4, 1, 2, 4>, (const void*)conv_split_ws_kernel<8, 1, 4, 8>};
         for (const void* k : ws) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
-        const void* w16[4] = {(const void*)conv_ws16_kernel<1, 1, NPD_WS16_NW>, (const void*)conv_ws16_kernel<1, 2, NPD_WS16_NW>,
-                              (const void*)conv_ws16_kernel<2, 1, NPD_WS16_NW>, (const void*)conv_ws16_kernel<2, 2, NPD_WS16_NW>};
+        const void* w16[5] = {(const void*)conv_ws16_kernel<1, 1, NPD_WS16_NW, 1>,
+                              (const void*)conv_ws16_kernel<1, 2, NPD_WS16_NW, 1>,
+                              (const void*)conv_ws16_kernel<2, 1, NPD_WS16_NW, 1>,
+                              (const void*)conv_ws16_kernel<2, 2, NPD_WS16_NW, 1>, (const void*)conv_ws16_kernel<4, 1, 8, 2>};
         for (const void* k : w16) NPD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
     }
@@ -1415,22 +1442,26 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                    c->img + L.boff, L.cin, L.cout, N, L.dil, L.res, am_out);
             else if (split && L.dil <= 4 && L.soff16 >= 0) {
                 // cin 32 / 64: 16x16x32 weight-stationary kernel, no channel parts; one 8-wave block per CU, a multiple of
-                // the 64-channel slice count; 128-position items where N allows
+                // the 64-channel slice count; 128-position items where N allows.  cin 128: two channel parts of 64,
+                // 64-position items
                 const int kbn = L.cin / 32;
-                const int Q = N % 128 == 0 && NPD_WS16_Q2 ? 2 : 1;
+                const int kp = kbn == 4 ? 2 : 1;
+                const int nw = kp == 2 ? 8 : NPD_WS16_NW;
+                const int Q = kp == 1 && N % 128 == 0 && NPD_WS16_Q2 ? 2 : 1;
                 const int nslices = (L.cout + 63) / 64;
                 const int64_t items = nb * (N / (64 * Q)) * nslices;
-                int64_t nblk = (int64_t)device_cu_count() * (8 / NPD_WS16_NW);
+                int64_t nblk = (int64_t)device_cu_count() * (8 / nw);
                 nblk -= nblk % nslices;
                 if (nblk > items) nblk = items;
                 if (nblk < nslices) nblk = nslices;
-                const size_t ls = ws16_lds_bytes(kbn, Q, L.dil);
+                const size_t ls = ws16_lds_bytes(kbn, Q, L.dil, kp);
                 const f4* wi = reinterpret_cast<const f4*>(c->img + L.soff16);
-#define NPD_WS16(KBV, QV)                                                                                          \
-    hipLaunchKernelGGL((conv_ws16_kernel<KBV, QV, NPD_WS16_NW>), dim3((unsigned)nblk), dim3(64 * NPD_WS16_NW), ls, s, \
-                       in, o, rsrc, wi, c->img + L.boff, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
-                if (kbn == 2) { if (Q == 2) NPD_WS16(2, 2); else NPD_WS16(2, 1); }
-                else { if (Q == 2) NPD_WS16(1, 2); else NPD_WS16(1, 1); }
+#define NPD_WS16(KBV, QV, NWV, KPV)                                                                                \
+    hipLaunchKernelGGL((conv_ws16_kernel<KBV, QV, NWV, KPV>), dim3((unsigned)nblk), dim3(64 * NWV), ls, s, in, o,    \
+                       rsrc, wi, c->img + L.boff, L.cout, N, L.dil, L.res, L.sw, am_in, am_out, nb, nslices)
+                if (kbn == 4) NPD_WS16(4, 1, 8, 2);
+                else if (kbn == 2) { if (Q == 2) NPD_WS16(2, 2, NPD_WS16_NW, 1); else NPD_WS16(2, 1, NPD_WS16_NW, 1); }
+                else { if (Q == 2) NPD_WS16(1, 2, NPD_WS16_NW, 1); else NPD_WS16(1, 1, NPD_WS16_NW, 1); }
 #undef NPD_WS16
             } else if (split && L.dil <= 4 && (L.cin <= 64 || L.cin == 128)) {
                 // weight-stationary persistent blocks: one per CU, a multiple of the 64-channel slice count.
