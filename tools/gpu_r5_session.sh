@@ -41,7 +41,7 @@ if [ -n "$BENCH" ]; then
 fi
 if [ -n "$PROF" ]; then
   export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r5 -o run -- python3 bench.py --no-traffic \
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r5 -o run -- python3 bench.py --full-json gpurun_out/bench_full_prof.json --no-traffic \
     --no-cpu-baseline --steps 5 --warmup 1 > gpurun_out/prof_r5.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof_r5.log; exit 1; }
   find gpurun_out/prof_r5 -name "*kernel_stats.csv" | head -3
 fi
