@@ -230,8 +230,8 @@ int npd_gru_destroy(npd_gru* gru);
 /*
  * npd_gru_create for either cell of rnn_all.py:69 (--rnn_type GRU | LSTM): cell 0 = GRU (npd_gru_create), cell 1 =
  * LSTM (nn.LSTM, gates i, f, g, o; the same weight order with 4F gate rows: weight_ih_l (4F, Din_l) | weight_hh_l (4F, F)
- * | bias_ih_l (4F) | bias_hh_l (4F) per layer, then linear.weight | linear.bias).  LSTM: fp32 (precision 0), hidden 32
- * (1 or 2 layers) or 64 (1 layer: at 2 layers its weights exceed the 160 KB LDS), y_input decoding (npd_gru_decode) or
+ * | bias_ih_l (4F) | bias_hh_l (4F) per layer, then linear.weight | linear.bias).  LSTM: fp32 (precision 0), hidden
+ * 32, 64, 128, 256 or 512, 1 or 2 layers (F = 512 with 2 layers: N <= 128, as the GRU), y_input decoding (npd_gru_decode) or
  * y_h0 decoding (npd_gru_decode_ex with y = NULL: h and c both start from h0, as get_h0 returns (x, x) for LSTM,
  * rnn_all.py:370-375); destroy with npd_gru_destroy.
  */

@@ -34,7 +34,7 @@ struct npd_gru {
     float* wy16;
     int64_t wy16_lo;
     int split16;   // its SplitT variant
-    int cell;      // 0 GRU, 1 LSTM (fp32, F <= 64)
+    int cell;      // 0 GRU, 1 LSTM (fp32)
 };
 
 namespace npd {
@@ -1678,6 +1678,206 @@ __global__ __launch_bounds__(64 * WideGeo<F>::NW) void gru_wide_kernel(const Arg
     }
 }
 
+// ------------------------------------------------------------------ LSTM cells beyond the LDS (F = 64 x 2, F >= 128)
+// gru_wide_kernel's scheme with LSTM cells: the build_image_lstm weight images (gate rows pre-scaled by their exp2
+// constants, biases as accumulator initialisation) stay in HBM / L2, the hidden states of the 32-codeword tile sit in
+// LDS in B-operand order, each wave owns HPW hidden tiles and computes all four gates (i, f, g, o) of them, and keeps
+// their cell states c in registers (accumulator layout = the tile's hidden units of the lane's codeword).
+template <int HPW>
+__device__ __forceinline__ void wide_chain4(const f4* __restrict__ W, int kg, int HT, int jt0, const f4* __restrict__ Bs,
+                                            int lane, f16v (&acc)[4][HPW]) {
+    f4 wc[4][HPW];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < HPW; ++j) wc[k][j] = W[((size_t)(k * HT + jt0 + j) * kg + 0) * 64 + lane];
+    for (int q = 0; q < kg; ++q) {
+        f4 wn[4][HPW];
+        if (q + 1 < kg) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) wn[k][j] = W[((size_t)(k * HT + jt0 + j) * kg + q + 1) * 64 + lane];
+        }
+        const f4 b = Bs[q * 64 + lane];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) acc[k][j] = mfma(wc[k][j][e], b[e], acc[k][j]);
+        if (q + 1 < kg) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) wc[k][j] = wn[k][j];
+        }
+    }
+}
+
+template <int F, int L>
+__global__ __launch_bounds__(64 * WideGeo<F>::NW) void lstm_wide_kernel(const Args a) {
+    using G = LGeo<F, L>;
+    using WG = WideGeo<F>;
+    constexpr int TT = G::TT, HT = G::HT, KG = G::KG, NW = WG::NW, HPW = WG::HPW;
+    extern __shared__ __attribute__((aligned(16))) f4 lds4[];
+    const int N = a.N;
+    f4* const Hs0 = lds4;
+    f4* const Hs1 = lds4 + (L == 2 ? F * 8 : 0);
+    f4* const Ys = lds4 + L * F * 8;
+    float* const part = reinterpret_cast<float*>(Ys + N * 8);
+    const float* img = a.img;
+    const f4* W0 = reinterpret_cast<const f4*>(img);
+    const f4* W1 = reinterpret_cast<const f4*>(img + (size_t)G::G_SIZE);
+    const f4* W2 = reinterpret_cast<const f4*>(img + 2 * (size_t)G::G_SIZE);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int half = lane >> 5;
+    const int col = lane & 31;
+    const int jt0 = wave * HPW;
+    const int ng = N / 8;
+    const int64_t ntiles = (a.B + 31) / 32;
+    auto cvec = [&](int off) -> f16v {
+        const f4* p = reinterpret_cast<const f4*>(img + off + half * 16);
+        const f4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        return f16v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                    x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+    };
+    constexpr float kT = -2.88539008177792681472f;  // tanh(c) = 2 sig2(kT c) - 1
+    // c' = sig(f) c + sig(i) tanh(g), h' = sig(o) tanh(c') on hidden tile jt; h' to the LDS state (B-operand order)
+    auto cell = [&](f4* Hs, int jt, f16v& c, f16v& h, const f16v& ai, const f16v& af, const f16v& ag, const f16v& ao) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float ig = sig2(ai[i]), fg = sig2(af[i]);
+            const float gg = fmaf(2.0f, sig2(ag[i]), -1.0f);
+            const float og = sig2(ao[i]);
+            c[i] = fmaf(fg, c[i], ig * gg);
+            h[i] = og * fmaf(2.0f, sig2(kT * c[i]), -1.0f);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Hs[(4 * jt + q) * 64 + lane] = f4{h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]};
+    };
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t cw = tile * 32 + col;
+        const bool valid = cw < a.B;
+        const int64_t cwc = valid ? cw : a.B - 1;
+        __syncthreads();  // the previous tile's last readers are done
+        if (a.y) {
+            const f4* yr = reinterpret_cast<const f4*>(a.y + cwc * N + half * (N / 2));
+            for (int q = wave; q < ng; q += NW) Ys[q * 64 + lane] = yr[q];
+        }
+        // h states in LDS and this wave's c states in registers: zero, or (y_h0) both from a.h0 (B, F L), element
+        // f L + l (get_h0 returns (x, x) for LSTM cells, rnn_all.py:370-375)
+        for (int i = threadIdx.x; i < L * F * 8; i += NW * 64) {
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (a.h0) {
+                const int l = i / (F * 8), idx = i - l * F * 8;
+                const int ln = idx & 63, jq = idx >> 6;
+                int64_t c = tile * 32 + (ln & 31);
+                if (c >= a.B) c = a.B - 1;
+                const float* hr = a.h0 + c * (int64_t)(F * L) + l;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = hr[hid_of(16 * (jq >> 2) + 4 * (jq & 3) + e, ln >> 5) * L];
+            }
+            lds4[i] = v;
+        }
+        f16v c0[HPW], c1[HPW], top[HPW];
+#pragma unroll
+        for (int j = 0; j < HPW; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float v0 = 0.0f, v1 = 0.0f;
+                if (a.h0) {
+                    const float* hr = a.h0 + cwc * (int64_t)(F * L) + hid_of(16 * (jt0 + j) + i, half) * L;
+                    v0 = hr[0];
+                    if constexpr (L == 2) v1 = hr[1];
+                }
+                c0[j][i] = v0;
+                c1[j][i] = v1;
+            }
+        __syncthreads();
+        float xb = 1.0f;
+        for (int ii = 0; ii < N; ++ii) {
+            const int jj = a.rev ? N - 1 - ii : ii;
+            const float xbe = half ? xb : 1.0f;
+            f16v acc[4][HPW];
+            // ================= layer 0: biases, W_ih0[:, :N] y, W_hh0 h0, the [1, x_i] k-step
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) acc[k][j] = cvec(G::OFF_CV + (k * HT + jt0 + j) * 32);
+            if (a.y) wide_chain4<HPW>(a.wy, ng, HT, jt0, Ys, lane, acc);
+            wide_chain4<HPW>(W0, KG, HT, jt0, Hs0, lane, acc);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < HPW; ++j) acc[k][j] = mfma(img[G::OFF_X + (k * HT + jt0 + j) * 64 + lane], xbe, acc[k][j]);
+            __syncthreads();  // every wave has read h0
+#pragma unroll
+            for (int j = 0; j < HPW; ++j) cell(Hs0, jt0 + j, c0[j], top[j], acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+            __syncthreads();  // h0' complete
+            if constexpr (L == 2) {
+                // ================= layer 1: biases, W_ih1 h0', W_hh1 h1
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int j = 0; j < HPW; ++j) acc[k][j] = cvec(G::OFF_CV + (TT + k * HT + jt0 + j) * 32);
+                wide_chain4<HPW>(W1, KG, HT, jt0, Hs0, lane, acc);
+                wide_chain4<HPW>(W2, KG, HT, jt0, Hs1, lane, acc);
+                __syncthreads();  // every wave has read h1
+#pragma unroll
+                for (int j = 0; j < HPW; ++j)
+                    cell(Hs1, jt0 + j, c1[j], top[j], acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+            }
+            // ================= output: Linear(F, 1) on the top layer, reduced over the waves in a fixed order
+            float p = 0.0f;
+#pragma unroll
+            for (int j = 0; j < HPW; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) p += img[G::OFF_WL + (half * HT + jt0 + j) * 16 + i] * top[j][i];
+            p += __shfl_xor(p, 32, 64);
+            if (half == 0) part[wave * 32 + col] = p;
+            __syncthreads();
+            float out = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) out += part[w * 32 + col];
+            out += a.b_lin;
+            const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
+            float d;
+            if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
+            else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+            if (wave == 0 && half == 0 && valid) {
+                a.decoded[cw * N + jj] = d;
+                if (a.logits) a.logits[cw * N + ii] = out;
+            }
+            const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+            xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
+        }
+    }
+}
+
+template <int F, int L>
+static int launch_lstm_wide(const Args& a, int N, hipStream_t s) {
+    using WG = WideGeo<F>;
+    auto kern = lstm_wide_kernel<F, L>;
+    const size_t lds = (size_t)wide_lds_bytes(N, F, L);
+    static bool attr = false;
+    if (!attr) {
+        NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        attr = true;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * WG::NW, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    const int64_t tiles = (a.B + 31) / 32;
+    const int grid = grid_for(tiles, occ, device_cu_count());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WG::NW), lds, s, a);
+    return launch_check("lstm_wide_kernel launch");
+}
+
 template <int F, int L>
 static int launch_wide(const Args& a, int N, hipStream_t s) {
     using WG = WideGeo<F>;
@@ -1706,9 +1906,10 @@ using namespace npd;
 
 static int create_lstm(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
                        npd_gru** out) {
-    NPD_ARG(F == 32 || F == 64, "npd_rnn_create: LSTM cells cover hidden sizes 32 and 64");
-    NPD_ARG(F == 32 || layers == 1,
-            "npd_rnn_create: an LSTM with hidden 64 and 2 layers needs 192 KB of LDS-resident weights (160 KB per CU)");
+    NPD_ARG(F == 32 || F == 64 || F == 128 || F == 256 || F == 512,
+            "npd_rnn_create: LSTM hidden size F must be 32, 64, 128, 256 or 512");
+    NPD_ARG(F <= 64 || gru::wide_lds_bytes(N, F, layers) <= 160 * 1024,
+            "npd_rnn_create: an LSTM with F = 512 and 2 layers needs N <= 128 (LDS holds both states and the tile's y)");
     NPD_ARG(precision == 0, "npd_rnn_create: LSTM cells run fp32 (precision 0)");
     const int Din = N + (onehot ? 2 : 1);
     int64_t expect = (int64_t)4 * F * Din + (int64_t)4 * F * F + 8 * F;
@@ -1717,9 +1918,15 @@ static int create_lstm(int N, int F, int layers, int onehot, const float* weight
     NPD_ARG(n_weights == expect, "npd_rnn_create: weight count does not match (LSTM, N, F, layers, onehot)");
     std::vector<float> img, wy;
     float b_lin = 0.0f;
-    if (F == 64) gru::build_image_lstm<64, 1>(weights, N, onehot, img, wy, b_lin);
-    else if (layers == 2) gru::build_image_lstm<32, 2>(weights, N, onehot, img, wy, b_lin);
-    else gru::build_image_lstm<32, 1>(weights, N, onehot, img, wy, b_lin);
+    // F = 32 (1-2 layers) and F = 64 x 1: LDS-resident weights (lstm_decode_kernel); else lstm_wide_kernel
+#define NPD_LSTM_IMG(FF, LL) gru::build_image_lstm<FF, LL>(weights, N, onehot, img, wy, b_lin)
+    if (F == 512) { if (layers == 2) NPD_LSTM_IMG(512, 2); else NPD_LSTM_IMG(512, 1); }
+    else if (F == 256) { if (layers == 2) NPD_LSTM_IMG(256, 2); else NPD_LSTM_IMG(256, 1); }
+    else if (F == 128) { if (layers == 2) NPD_LSTM_IMG(128, 2); else NPD_LSTM_IMG(128, 1); }
+    else if (F == 64) { if (layers == 2) NPD_LSTM_IMG(64, 2); else NPD_LSTM_IMG(64, 1); }
+    else if (layers == 2) NPD_LSTM_IMG(32, 2);
+    else NPD_LSTM_IMG(32, 1);
+#undef NPD_LSTM_IMG
     npd_gru* g = new (std::nothrow) npd_gru;
     if (!g) return fail(NPD_ENOMEM, "npd_rnn_create: out of memory");
     memset(g, 0, sizeof(*g));
@@ -1874,7 +2081,11 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
         if (is_info[i]) a.info[i >> 5] |= 1u << (i & 31);
     hipStream_t s = (hipStream_t)stream;
     if (g->cell == 1) {
-        if (g->F == 64) return gru::launch_lstm<64, 1>(a, s);
+        const int N = g->N;
+        if (g->F == 512) return g->layers == 2 ? gru::launch_lstm_wide<512, 2>(a, N, s) : gru::launch_lstm_wide<512, 1>(a, N, s);
+        if (g->F == 256) return g->layers == 2 ? gru::launch_lstm_wide<256, 2>(a, N, s) : gru::launch_lstm_wide<256, 1>(a, N, s);
+        if (g->F == 128) return g->layers == 2 ? gru::launch_lstm_wide<128, 2>(a, N, s) : gru::launch_lstm_wide<128, 1>(a, N, s);
+        if (g->F == 64) return g->layers == 2 ? gru::launch_lstm_wide<64, 2>(a, N, s) : gru::launch_lstm<64, 1>(a, s);
         return g->layers == 2 ? gru::launch_lstm<32, 2>(a, s) : gru::launch_lstm<32, 1>(a, s);
     }
     if (g->precision != 0) {

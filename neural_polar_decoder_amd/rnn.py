@@ -103,11 +103,11 @@ class RNN_Model(nn.Module):
     def fused_supported(self, decoding_type="y_input") -> bool:
         common = (self.output_size == 1 and self.out_linear_depth == 1 and not self.bidirectional
                   and isinstance(self.layernorm, nn.Identity) and self.num_rnn_layers in (1, 2))
-        if self.rnn_type == "LSTM":  # fp32 lstm_decode_kernel: hidden 32, or 64 with one layer (LDS-resident weights)
-            shape = self.feature_size == 32 or (self.feature_size == 64 and self.num_rnn_layers == 1)
+        if self.rnn_type == "LSTM":  # fp32: lstm_decode_kernel (F 32, F 64 x 1 layer), lstm_wide_kernel (the rest)
+            shape = self.feature_size in (32, 64, 128, 256, 512)
             if decoding_type == "y_h0":  # (h, c) both start from get_h0's x (rnn_all.py:370-375)
                 return common and shape and self._ymlp_ok(self.num_rnn_layers * self.feature_size)
-            return common and shape and decoding_type == "y_input" and self.y_depth == 0
+            return common and shape and decoding_type == "y_input" and (self.y_depth == 0 or self._ymlp_ok(self.y_size))
         base = common and self.rnn_type == "GRU" and self.feature_size in (32, 64, 128, 256, 512)
         if decoding_type == "y_h0":
             return base and self._ymlp_ok(self.num_rnn_layers * self.feature_size)

@@ -29,7 +29,9 @@ def test_lstm_shapes_accepted():
     from neural_polar_decoder_amd.rnn import RNN_Model
     assert RNN_Model("LSTM", 66, 64, 1, 1, 64, 0, 0).fused_supported("y_input")
     assert RNN_Model("LSTM", 34, 32, 1, 2, 32, 0, 0).fused_supported("y_input")
-    assert not RNN_Model("LSTM", 66, 64, 1, 2, 64, 0, 0).fused_supported("y_input")  # 192 KB of weights > LDS
+    assert RNN_Model("LSTM", 66, 64, 1, 2, 64, 0, 0).fused_supported("y_input")  # lstm_wide_kernel (round 5)
+    assert RNN_Model("LSTM", 66, 256, 1, 2, 64, 0, 0).fused_supported("y_input")
+    assert not RNN_Model("LSTM", 66, 96, 1, 1, 64, 0, 0).fused_supported("y_input")
     assert RNN_Model("LSTM", 2, 32, 1, 1, 32, 64, 2).fused_supported("y_h0")  # y_h0: (h, c) = (x, x), round 5
-    assert not RNN_Model("LSTM", 2, 64, 1, 2, 64, 64, 2).fused_supported("y_h0")
+    assert RNN_Model("LSTM", 2, 64, 1, 2, 64, 64, 2).fused_supported("y_h0")
     del torch
