@@ -45,20 +45,33 @@ def reference_loop(net, y, N, info):
     return dec.numpy(), lg.numpy()
 
 
-@pytest.mark.parametrize("name,n", [("trained_crisp_64_32", 1 << 14), ("trained_crisp_32_16", 1 << 15)])
+@pytest.mark.parametrize("name,n", [("trained_crisp_64_32", 1 << 14), ("trained_crisp_32_16", 1 << 15),
+                                    ("seeded_pac_128_64", 1 << 12)])
 def test_fp16x3_error_matches_fp32_kernel_against_float64(name, n):
+    """seeded_pac_128_64: configs[3]'s PAC(128,64) CRISP GRU as the bench builds it (no trained PAC net exists,
+    DESIGN.md 2b: montecarlo.seeded_crisp, seed 0), decoding PAC words -- the shape (N = 128) the bench's pac_gru
+    record runs on the split kernel."""
+    import argparse
     from oracle import oracle as O
-    from neural_polar_decoder_amd import reference_polar_code
+    from neural_polar_decoder_amd import PAC, reference_polar_code
+    from neural_polar_decoder_amd.montecarlo import seeded_crisp
     from neural_polar_decoder_amd.rnn import RNN_decoder, RNN_Model
-    d = trained_fixture(name)
-    N, K, F, L = int(d["N"]), int(d["K"]), int(d["F"]), int(d["layers"])
-    info = np.asarray(d["info"], np.int64)
-    sd = {k[2:]: np.asarray(d[k]) for k in d.files if k.startswith("w.")}
+    if name == "seeded_pac_128_64":
+        code = PAC(argparse.Namespace(target_K=64), 128, 64, 91)
+        seeded, _ = seeded_crisp(code, 64, 2, seed=0, device="cpu")
+        N, F, L = 128, 64, 2
+        info = np.asarray(code.B, np.int64)
+        sd = {k: v.detach().numpy() for k, v in seeded.state_dict().items()}
+    else:
+        d = trained_fixture(name)
+        N, K, F, L = int(d["N"]), int(d["K"]), int(d["F"]), int(d["layers"])
+        info = np.asarray(d["info"], np.int64)
+        sd = {k[2:]: np.asarray(d[k]) for k in d.files if k.startswith("w.")}
+        code = reference_polar_code(N, K)
     net = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).eval()
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     gnet = RNN_Model("GRU", N + 2, F, 1, L, N, 0, 0).to(DEV).eval()
     gnet.load_state_dict(net.state_dict())
-    code = reference_polar_code(N, K)
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     errs = {k: [] for k in ("reference", "fp32", "fp16x3")}
     flips = {k: 0 for k in errs}
