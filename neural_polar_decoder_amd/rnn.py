@@ -21,7 +21,7 @@ class RNN_Model(nn.Module):
     """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts nets with output_size 1,
     out_linear_depth 1, unidirectional, no layernorm: GRU with decoding_type 'y_input' -- y_depth 0 (the CRISP
     scripts, rnn_all.py:250-253) or --use_ynn's y-MLP of N outputs feeding the GRU in place of y (rnn_all.py:1319-1320,
-    :533-536) -- or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, no skip); LSTM
+    :533-536) -- or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, with or without skip); LSTM
     (rnn_all.py:69) with 'y_input' or 'y_h0', fp32, hidden 32 or hidden 64 with one layer."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
@@ -89,8 +89,9 @@ class RNN_Model(nn.Module):
             x = layer(x) if ii == self.y_depth else self.act(layer(x))
         return x
 
-    def _ymlp_ok(self, out_size):
-        return (hasattr(self, "y_linears") and not self.skip and self.activation in self.ACTS
+    def _ymlp_ok(self, out_size, allow_skip=False):
+        # skip (get_h0 only, rnn_all.py:369-370): the MLP's y_output_size - y_size outputs follow y itself
+        return (hasattr(self, "y_linears") and (allow_skip or not self.skip) and self.activation in self.ACTS
                 and self.y_output_size == out_size)
 
     def forward(self, input, hidden, Fy=None):
@@ -106,11 +107,11 @@ class RNN_Model(nn.Module):
         if self.rnn_type == "LSTM":  # fp32: lstm_decode_kernel (F 32, F 64 x 1 layer), lstm_wide_kernel (the rest)
             shape = self.feature_size in (32, 64, 128, 256, 512)
             if decoding_type == "y_h0":  # (h, c) both start from get_h0's x (rnn_all.py:370-375)
-                return common and shape and self._ymlp_ok(self.num_rnn_layers * self.feature_size)
+                return common and shape and self._ymlp_ok(self.num_rnn_layers * self.feature_size, allow_skip=True)
             return common and shape and decoding_type == "y_input" and (self.y_depth == 0 or self._ymlp_ok(self.y_size))
         base = common and self.rnn_type == "GRU" and self.feature_size in (32, 64, 128, 256, 512)
         if decoding_type == "y_h0":
-            return base and self._ymlp_ok(self.num_rnn_layers * self.feature_size)
+            return base and self._ymlp_ok(self.num_rnn_layers * self.feature_size, allow_skip=True)
         # y_input: y itself (y_depth 0) or --use_ynn's Fy = get_Fy(y) with N outputs (rnn_all.py:533-536)
         return base and (self.y_depth == 0 or self._ymlp_ok(self.y_size))
 
@@ -220,8 +221,10 @@ class RNN_decoder:
         return (dec, _lib.home(logits, y_in)) if return_logits else dec
 
     def _h0(self, net, y):
-        """(B, F * layers) initial states: get_h0's MLP, kept alive past the stream-ordered decode by the caller."""
-        return _ymlp_forward(net, y)
+        """(B, F * layers) initial states: get_h0's MLP (y first when the net was built with skip, rnn_all.py:369-370),
+        kept alive past the stream-ordered decode by the caller."""
+        x = _ymlp_forward(net, y)
+        return torch.cat([y, x], 1).contiguous() if net.skip else x
 
 
 def _ymlp_forward(net: RNN_Model, y: torch.Tensor) -> torch.Tensor:

@@ -478,6 +478,38 @@ def gen_gru_yh0():
              **{"w." + k: v for k, v in sd.items()})
 
 
+def gen_gru_yh0_skip():
+    """gen_gru_yh0 with RNN_Model(..., skip=True) (--use_skip): get_h0 puts y in front of the y-MLP's F L - N outputs
+    before the reshape (rnn_all.py:369-370)."""
+    cases = [("gru_yh0_polar_32_16_skip", 32, 16, 64, 2, True, False, "relu", 64, 2, 256, 3006)]
+    for name, N, K, F, L, onehot, rev, act, yh, yd, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        net = rnn_m.RNN_Model("GRU", 1 + int(onehot), F, 1, L, N, yh, yd, act, 0.0, True)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_h0", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits, h0s = [], [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+                h0 = net.get_h0(y)  # (L, B, F)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+            h0s.append(h0.permute(1, 2, 0).reshape(y.shape[0], -1).numpy())  # x layout: f * L + l
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), h0x=np.concatenate(h0s), info=info, N=N, K=K, F=F, layers=L,
+             onehot=int(onehot), rev=int(rev), activation=np.bytes_(act), y_hidden=yh, y_depth=yd, skip=1,
+             **{"w." + k: v for k, v in sd.items()})
+
+
 def gen_gru_ynn():
     """decoding_type 'y_input' with --use_ynn (rnn_all.py:1319-1320: y_output_size = N, the y-MLP's output replaces y as
     the GRU input; decode test branch rnn_all.py:533-536 Fy = net.get_Fy(y), then the y_input loop on [Fy, onehot]):
@@ -623,6 +655,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_ynn", "lstm", "lstm_yh0", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "lstm", "lstm_yh0", "conv"]
     for w in which:
         globals()["gen_" + w]()

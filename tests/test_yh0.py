@@ -2,7 +2,7 @@
 (oracle.ymlp_f64 + gru_decode_f64 with an initial state) and this package's RNN_Model.get_h0 against the reference's
 golden decisions, logits and initial states (tests/golden/gen_golden.py gen_gru_yh0: PyTorch-default seeded weights,
 five nets covering every activation, 1 / 2 layers, F 32 / 64 / 128, one-hot and sign inputs, reverse order,
-y_depth 1..4)."""
+y_depth 1..4; gen_gru_yh0_skip: a skip y-MLP)."""
 import numpy as np
 import pytest
 import torch
@@ -10,7 +10,12 @@ import torch
 from conftest import golden
 
 CASES = ["gru_yh0_polar_64_32", "gru_yh0_polar_32_16_f128_relu_rev", "gru_yh0_polar_16_8_l1_tanh_noonehot",
-         "gru_yh0_polar_32_16_elu_d1", "gru_yh0_polar_16_8_sigmoid"]
+         "gru_yh0_polar_32_16_elu_d1", "gru_yh0_polar_16_8_sigmoid", "gru_yh0_polar_32_16_skip"]
+
+
+def skip_of(d):
+    """gen_gru_yh0_skip: RNN_Model(..., skip=True) -- get_h0 puts y in front of the MLP output (rnn_all.py:369-370)."""
+    return bool(int(d["skip"])) if "skip" in d.files else False
 
 
 def load(name):
@@ -26,6 +31,8 @@ def test_oracle_yh0_matches_reference(oracle, name):
     act = bytes(d["activation"]).decode()
     y = d["y"]
     x = oracle.ymlp_f64(y, sd, act, int(d["y_depth"]))
+    if skip_of(d):
+        x = np.concatenate([y.astype(np.float64), x], 1)
     assert np.abs(x - d["h0x"]).max() < 1e-5  # the reference's fp32 MLP against float64
     dec, lg = oracle.gru_decode_f64(y, sd, N, F, L, d["info"], onehot=bool(d["onehot"]), h0x=x, rev=bool(d["rev"]))
     ref = d["decoded"]
@@ -45,7 +52,7 @@ def test_rnn_model_get_h0_matches_reference(name):
     d, sd = load(name)
     N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
     net = RNN_Model("GRU", 1 + int(d["onehot"]), F, 1, L, N, int(d["y_hidden"]), int(d["y_depth"]),
-                    bytes(d["activation"]).decode(), 0.0, False)
+                    bytes(d["activation"]).decode(), 0.0, skip_of(d))
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     assert net.fused_supported("y_h0") and not net.fused_supported("y_input")
     with torch.no_grad():

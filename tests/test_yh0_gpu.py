@@ -12,8 +12,8 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 CASES = ["gru_yh0_polar_64_32", "gru_yh0_polar_32_16_f128_relu_rev", "gru_yh0_polar_16_8_l1_tanh_noonehot",
-         "gru_yh0_polar_32_16_elu_d1", "gru_yh0_polar_16_8_sigmoid"]
-SPLIT_OK = {"gru_yh0_polar_64_32", "gru_yh0_polar_32_16_elu_d1"}
+         "gru_yh0_polar_32_16_elu_d1", "gru_yh0_polar_16_8_sigmoid", "gru_yh0_polar_32_16_skip"]
+SPLIT_OK = {"gru_yh0_polar_64_32", "gru_yh0_polar_32_16_elu_d1", "gru_yh0_polar_32_16_skip"}
 
 
 def build(name, precision="fp32"):
@@ -21,8 +21,9 @@ def build(name, precision="fp32"):
     d = golden(f"{name}.npz")
     sd = {k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w.")}
     N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
+    skip = bool(int(d["skip"])) if "skip" in d.files else False  # gen_gru_yh0_skip (rnn_all.py:369-370)
     net = RNN_Model("GRU", 1 + int(d["onehot"]), F, 1, L, N, int(d["y_hidden"]), int(d["y_depth"]),
-                    bytes(d["activation"]).decode(), 0.0, False).to(DEV).eval()
+                    bytes(d["activation"]).decode(), 0.0, skip).to(DEV).eval()
     net.load_state_dict(sd)
     dec = RNN_decoder("y_h0", N, d["info"], onehot=bool(d["onehot"]), reverse_order=bool(d["rev"]),
                       precision=precision)
@@ -48,9 +49,8 @@ def test_yh0_decode_matches_reference(name, precision):
 
 @pytest.mark.parametrize("name", CASES)
 def test_yh0_mlp_matches_reference(name):
-    from neural_polar_decoder_amd.rnn import _ymlp_forward
-    d, net, _ = build(name)
-    x = _ymlp_forward(net, torch.from_numpy(d["y"]).to(DEV)).cpu().numpy()
+    d, net, dec = build(name)
+    x = dec._h0(net, torch.from_numpy(d["y"]).to(DEV)).cpu().numpy()  # the MLP (and skip's y in front) on the GPU
     assert np.abs(x - d["h0x"]).max() < 1e-5
 
 
