@@ -507,18 +507,20 @@ static size_t ws_lds_bytes(int ng, int Q, int ks, int nw, int dil) {
     return slabs + (ks > 1 ? (size_t)nw * rs * 16 * 64 * 4 : 0);
 }
 
-// ------------------------------------------------------------------------------ conv layer, fp16x3, no channel parts
-// cin = 32 KB (KB = 1, 2): the weight-stationary kernel on v_mfma_f32_16x16x32_f16.  A 16-row tile of output channels
-// needs 7 taps x KB K blocks x (hi, lo) A fragments = 56 KB registers per wave (112 at cin 64), so each wave holds ALL
-// input channels of its 16 output channels -- no channel parts, no partial-sum exchange through LDS and no second
-// barrier, which is what held conv_split_ws_kernel's 64-channel layers at ~0.4 of the MFMA rate (its 32-row tiles need
-// 224 registers for all 64 channels, hence the 2 parts).  8 waves = 4 x 16 output channels (a 64-channel slice) x 2
-// position halves of a 64 Q-position item (Q 16-position tiles per wave, TPW = 2 Q).  16x16x32 operand map (lane
-// l = 16 g + c): A[row c][k 8g + j], B[k 8g + j][col c], D[row 4g + i][col c]; k of K block kb = channel 32 kb + k, so a
-// B fragment is 8 channels of one slab row: one ds_read_b128 per plane from the double-buffered hi / lo slab, and the
-// accumulator's 4 registers are 4 consecutive channels of one position (16-B epilogue stores).  The next item's slab is
-// fetched into registers before the MFMAs and split into the other buffer after them, the residual of this item
-// before them; one barrier per item.
+// ------------------------------------------------------------------------------ conv layer, fp16x3, 16-row tiles
+// cin = 32 KB (KB = 1, 2, 4): the weight-stationary kernel on v_mfma_f32_16x16x32_f16.  A 16-row tile of output
+// channels needs 7 taps x KB K blocks x (hi, lo) A fragments = 56 KB registers per wave (112 at cin 64), so at cin <= 64
+// each wave holds ALL input channels of its 16 output channels -- no channel parts, no partial-sum exchange through LDS
+// and no second barrier, which is what held conv_split_ws_kernel's 64-channel layers at ~0.4 of the MFMA rate (its
+// 32-row tiles need 224 registers for all 64 channels, hence the 2 parts).  8 waves = 4 x 16 output channels (a
+// 64-channel slice) x 2 position halves of a 64 Q-position item (TPW = 2 Q 16-position tiles per wave); at cin 128
+// (KP = 2) the two halves are channel parts instead, each finishing half of the item's tiles with the other's 16-B
+// partial sums from LDS.  16x16x32 operand map (lane l = 16 g + c): A[row c][k 8g + j], B[k 8g + j][col c],
+// D[row 4g + i][col c]; k of K block kb = channel 32 kb + k, so a B fragment is 8 channels of one slab row: one
+// ds_read_b128 per plane from the double-buffered hi / lo slab, and the accumulator's 4 registers are 4 consecutive
+// channels of one position (16-B epilogue stores).  The next item's slab is fetched into registers before the MFMAs
+// and split into the other buffer after them, the residual of this item before them; one barrier per item (two with
+// channel parts).
 __device__ __forceinline__ f4 mfma16x32(const hf8& a, const hf8& b, const f4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
