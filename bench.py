@@ -594,14 +594,14 @@ def lse_leg(code, dev, y, snr, world, timer):
             "config": "Polar(64,32) sc_decode exact-LSE (polar.py:209-279), 2 dB, msg_hat out"}
 
 
-CONV_PRECISION_JSON = os.path.join(ROOT, "profiles", "round4", "conv_precision.json")
+CONV_PRECISION_JSON = os.path.join(ROOT, "profiles", "round5", "conv_precision.json")
 
 
 def conv_leg(dev, rank, world, timer, batch=8192):
     """configs[4]: Polar(256,128) convNet decoder, embed 128 (run_alt.sh), seeded random weights; batch per GPU,
     whole-job codewords/s.  The record runs the fp16x3 path (conv and Linear layers on v_mfma_f32_32x32x16_f16, hi + lo
     split, fp32 accumulation): measured, its logit error against a float64 forward is below the fp32 path's at every
-    percentile (profiles/round4/conv_precision.json, tools/conv_precision.py); tests/test_conv_gpu.py enforces the looser
+    percentile (profiles/round5/conv_precision.json, tools/conv_precision.py); tests/test_conv_gpu.py enforces the looser
     bound of 1.5x the fp32 path's error at p50 / p99 / p99.9 and 2x at the maximum; the fp32 MFMA path is reported beside
     it (fp32_path)."""
     from neural_polar_decoder_amd import reference_polar_code
@@ -631,7 +631,7 @@ def conv_leg(dev, rank, world, timer, batch=8192):
                          "peak": FP16_PEAK_TF, "frac": 3 * p16["tf"] / FP16_PEAK_TF},
             "max_abs_logit_diff_vs_fp32": float((p16["lg"] - p32["lg"]).abs().max()),
             "precision_evidence": None if prec_table is None else {
-                "source": "profiles/round4/conv_precision.json (tools/conv_precision.py)",
+                "source": "profiles/round5/conv_precision.json (tools/conv_precision.py, final round-5 kernels)",
                 "abs_logit_error_vs_float64": {c: {k: {q: v[k][q] for q in ("p50", "p99", "p99.9", "max")}
                                                    for k in ("reference", "fp32", "fp16x3")}
                                                for c, v in prec_table["cases"].items()}},
