@@ -102,33 +102,53 @@ class RNN_Model(nn.Module):
         return decoded.view(-1, self.output_size), hidden
 
     def fused_supported(self, decoding_type="y_input") -> bool:
-        common = (self.output_size == 1 and self.out_linear_depth == 1 and not self.bidirectional
+        common = (self.output_size == 1 and self.out_linear_depth == 1
                   and isinstance(self.layernorm, nn.Identity) and self.num_rnn_layers in (1, 2))
+        fe = self.feature_size * (2 if self.bidirectional else 1)  # a bidirectional net runs as the 2F cell
         if self.rnn_type == "LSTM":  # fp32: lstm_decode_kernel (F 32, F 64 x 1 layer), lstm_wide_kernel (the rest)
-            shape = self.feature_size in (32, 64, 128, 256, 512)
+            shape = fe in (32, 64, 128, 256, 512)
             if decoding_type == "y_h0":  # (h, c) both start from get_h0's x (rnn_all.py:370-375)
-                return common and shape and self._ymlp_ok(self.num_rnn_layers * self.feature_size, allow_skip=True)
+                return common and shape and self._ymlp_ok(self.num_rnn_layers * fe, allow_skip=True)
             return common and shape and decoding_type == "y_input" and (self.y_depth == 0 or self._ymlp_ok(self.y_size))
-        base = common and self.rnn_type == "GRU" and self.feature_size in (32, 64, 128, 256, 512)
+        base = common and self.rnn_type == "GRU" and fe in (32, 64, 128, 256, 512)
         if decoding_type == "y_h0":
-            return base and self._ymlp_ok(self.num_rnn_layers * self.feature_size, allow_skip=True)
+            return base and self._ymlp_ok(self.num_rnn_layers * fe, allow_skip=True)
         # y_input: y itself (y_depth 0) or --use_ynn's Fy = get_Fy(y) with N outputs (rnn_all.py:533-536)
         return base and (self.y_depth == 0 or self._ymlp_ok(self.y_size))
 
 
 def pack_gru_weights(net: nn.Module, layers: int, y_cols: int = 0) -> np.ndarray:
     """Flatten the state dict in the order of include/npd.h npd_gru_create; y_cols > 0 ('y_h0'): weight_ih_l0 gets
-    y_cols zero columns in front (the y_input layout with no y)."""
-    sd = net.state_dict()
+    y_cols zero columns in front (the y_input layout with no y).
+
+    A bidirectional net (--bidirectional: nn.GRU / nn.LSTM over the one-step sequence, rnn_all.py:307) is packed as the
+    one-directional cell of hidden 2F it is on that sequence: unit dir F + f of the packed cell is unit f of direction
+    dir, so per gate the forward rows come first, then the reverse ones; both directions read the same layer input
+    (layer 0: [y, bit]; layer l > 0: the previous layer's [h_fwd, h_rev] = the packed state); W_hh is block-diagonal
+    (each direction's recurrence sees only its own state -- the zero blocks add exact zeros); linear.weight already
+    runs over [h_fwd, h_rev] (rnn_all.py:335)."""
+    sd = {k: v.detach().float().cpu().numpy() for k, v in net.state_dict().items()}
+    F = net.feature_size
+    G = 4 if net.rnn_type == "LSTM" else 3
     parts = []
     for l in range(layers):
         for nm in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
-            w = sd[f"rnn.{nm}_l{l}"].detach().float().cpu().numpy()
+            w = sd[f"rnn.{nm}_l{l}"]
+            if net.bidirectional:
+                wr = sd[f"rnn.{nm}_l{l}_reverse"]
+                if nm == "weight_hh":  # block-diagonal: (G 2F, 2F)
+                    z = np.zeros((G, F, F), np.float32)
+                    fw = np.concatenate([w.reshape(G, F, F), z], 2)
+                    rv = np.concatenate([z, wr.reshape(G, F, F)], 2)
+                else:  # rows of each gate: forward then reverse
+                    fw, rv = w.reshape(G, F, -1), wr.reshape(G, F, -1)
+                w = np.concatenate([fw, rv], 1).reshape(2 * G * F, -1).squeeze(-1) if w.ndim == 1 else \
+                    np.concatenate([fw, rv], 1).reshape(2 * G * F, -1)
             if nm == "weight_ih" and l == 0 and y_cols:
                 w = np.concatenate([np.zeros((w.shape[0], y_cols), np.float32), w], 1)
             parts.append(w.ravel())
-    parts.append(sd["linear.weight"].detach().float().cpu().numpy().ravel())
-    parts.append(sd["linear.bias"].detach().float().cpu().numpy().ravel())
+    parts.append(sd["linear.weight"].ravel())
+    parts.append(sd["linear.bias"].ravel())
     return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
 
 
@@ -182,7 +202,7 @@ class RNN_decoder:
             self._cache.clear()
             W = pack_gru_weights(net, net.num_rnn_layers, self.N if self.decoding_type == "y_h0" else 0)
             with torch.cuda.device(device):
-                h = _GruHandle(self.N, net.feature_size, net.num_rnn_layers, self.onehot, W,
+                h = _GruHandle(self.N, net.feature_size * (2 if net.bidirectional else 1), net.num_rnn_layers, self.onehot, W,
                                self.PRECISIONS[self.precision], 1 if net.rnn_type == "LSTM" else 0)
             self._cache[key] = h
         return h
@@ -224,7 +244,11 @@ class RNN_decoder:
         """(B, F * layers) initial states: get_h0's MLP (y first when the net was built with skip, rnn_all.py:369-370),
         kept alive past the stream-ordered decode by the caller."""
         x = _ymlp_forward(net, y)
-        return torch.cat([y, x], 1).contiguous() if net.skip else x
+        x = torch.cat([y, x], 1).contiguous() if net.skip else x
+        if net.bidirectional:  # get_h0's state (l, dir) of unit f is x[f 2L + 2l + dir]; the 2F cell wants (dir F + f) L + l
+            B, F, L = x.shape[0], net.feature_size, net.num_rnn_layers
+            x = x.view(B, F, L, 2).permute(0, 3, 1, 2).contiguous().view(B, 2 * F * L)
+        return x
 
 
 def _ymlp_forward(net: RNN_Model, y: torch.Tensor) -> torch.Tensor:

@@ -610,6 +610,44 @@ def gen_lstm():
              **{"w." + k: v for k, v in sd.items()})
 
 
+
+def gen_rnn_bi():
+    """--bidirectional (rnn_all.py:307: nn.GRU / nn.LSTM with bidirectional=True over the one-step sequence; decode
+    hidden = zeros(2 L, B, F), rnn_all.py:442; y_h0: get_h0's reshape to (2 L, B, F), rnn_all.py:371): seeded
+    PyTorch-default weights, Polar codes, reference encoder / channel at 0-4 dB, logits by a hook on net.linear."""
+    cases = [("gru_bi_polar_32_16_f32_l2", "GRU", 32, 16, 32, 2, True, False, "y_input", 0, 0, 256, 6001),
+             ("gru_bi_polar_16_8_f64_l1_rev", "GRU", 16, 8, 64, 1, True, True, "y_input", 0, 0, 256, 6002),
+             ("lstm_bi_polar_16_8_f16_l2", "LSTM", 16, 8, 16, 2, True, False, "y_input", 0, 0, 256, 6003),
+             ("gru_yh0_bi_polar_32_16", "GRU", 32, 16, 32, 2, True, False, "y_h0", 64, 2, 256, 6004)]
+    for name, cell, N, K, F, L, onehot, rev, dt, yh, yd, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        din = (N if dt == "y_input" else 0) + 1 + int(onehot)
+        net = rnn_m.RNN_Model(cell, din, F, 1, L, N, yh, yd, "relu", 0.0, False, bidirectional=True)
+        net.eval()
+        dec = rnn_m.RNN_decoder(dt, N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits, h0s = [], [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+                if dt == "y_h0":
+                    h0 = net.get_h0(y)  # (2 L, B, F), index layer 2 + direction
+                    h0s.append(h0.permute(1, 2, 0).reshape(y.shape[0], -1).numpy())  # x layout: f 2L + j
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        extra = dict(h0x=np.concatenate(h0s), y_hidden=yh, y_depth=yd, activation=np.bytes_("relu")) if h0s else {}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, layers=L, onehot=int(onehot), rev=int(rev),
+             cell=np.bytes_(cell), decoding_type=np.bytes_(dt), **extra, **{"w." + k: v for k, v in sd.items()})
+
 # ------------------------------------------------------------------------------------------- conv
 def conv_weights_from_seed(embed, N, seed):
     """Documented deterministic generator (mirrored in tests/conftest.py): PCG64(seed); each parameter,
@@ -655,6 +693,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "lstm", "lstm_yh0", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "lstm", "lstm_yh0", "rnn_bi", "conv"]
     for w in which:
         globals()["gen_" + w]()
