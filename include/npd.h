@@ -257,6 +257,20 @@ int npd_gru_decode(const npd_gru* gru, const float* y, const uint8_t* is_info, i
 int npd_gru_decode_ex(const npd_gru* gru, const float* y, const float* h0, const uint8_t* is_info, int reverse,
                       const float* gt, float* decoded, float* logits, int64_t B, void* stream);
 /*
+ * The eval loop's GRU half over an SNR sweep (rnn_all.py:853-880: at each SNR point decoded = RNN_decoder.decode(y_s),
+ * then errors_ber / errors_bler(msg, decoded[:, info]), rnn_all.py:874-879, utils.py:17-51): y is (n_seg, B, N), one
+ * segment of received words per SNR point; msg (B, K) the message bits of the B codewords (the same messages in every
+ * segment: the Monte-Carlo driver's message stream is keyed by codeword, not SNR); cols (K, HOST) the decoded columns
+ * compared with msg's columns.  counters (n_seg, 2) += [bit errors, block errors] of each segment -- equal, count for
+ * count, to npd_gru_decode_ex + npd_count_errors_cols per segment.  decoded (n_seg, B, N) is optional for the
+ * 16-codeword split kernel (F = 64, 2 layers, N % 32 == 0, precision != 0), which decodes and counts every segment in
+ * ONE launch (errors counted in the decision epilogue, one atomic pair per wave and segment); other handles run one
+ * decode + one count per segment and need decoded.  y_input decoding, no gt, no logits.
+ */
+int npd_gru_decode_count_sweep(const npd_gru* gru, int n_seg, const float* y, const uint8_t* is_info, int reverse,
+                               const float* msg, int K, const int32_t* cols, float* decoded, int64_t B,
+                               unsigned long long* counters, void* stream);
+/*
  * One layer of RNN_Model.get_h0 / get_Fy (rnn_all.py:362-385): out (B, Nout) = act(x (B, K) W^T + bias), W (Nout, K)
  * row-major, all device fp32, k summed in order.  act: 0 linear, 1 relu, 2 selu, 3 elu, 4 tanh, 5 sigmoid
  * (RNN_Model.act, rnn_all.py:346-360).  get_h0 follows layer ii with act iff ii != y_depth (rnn_all.py:364-368): every

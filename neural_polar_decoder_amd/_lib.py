@@ -56,6 +56,8 @@ SIGNATURES = [
     ("npd_rnn_create", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
     ("npd_gru_decode_ex", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64,
                                   c_void_p]),
+    ("npd_gru_decode_count_sweep", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                           c_void_p, c_i64, c_void_p, c_void_p]),
     ("npd_ymlp_layer", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int, c_void_p]),
     ("npd_conv_create", c_int, [c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
     ("npd_conv_destroy", c_int, [c_void_p]),

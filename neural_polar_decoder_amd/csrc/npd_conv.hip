@@ -940,13 +940,17 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
     if (loader) {
         const int lt = tid - 256;
         // per-lane byte offsets (fixed for the launch) against wave-uniform K-block bases: one 32-bit address register
-        // per load, no 64-bit address arithmetic per K block
+        // per load, no 64-bit address arithmetic per K block.  The offsets are relative to the block's first row of X
+        // and of W (64-bit bases), so they stay below 128 K 4 B < 2^28 at the largest accepted K = 512 x 1024
+        const char* const xblk = reinterpret_cast<const char*>(X) + (size_t)m0 * K * 4;
+        const char* const hblk = reinterpret_cast<const char*>(Whi) + (size_t)j0 * K * 2;
+        const char* const lblk = reinterpret_cast<const char*>(Wlo) + (size_t)j0 * K * 2;
         uint32_t offA[UA], offB[UB], ldsA[UA], ldsB[UB];
 #pragma unroll
         for (int u = 0; u < UA; ++u) {
             const int idx = lt + NL * u;
             const int r = idx / A4, c4 = (idx % A4) * 4;
-            const int mr = min(m0 + r, M - 1);
+            const int mr = min(m0 + r, M - 1) - m0;  // row within the block: < 128
             offA[u] = (uint32_t)(((int64_t)mr * K + c4) * 4);
             ldsA[u] = (uint32_t)(r * GSW + c4);
         }
@@ -954,15 +958,15 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
         for (int u = 0; u < UB; ++u) {
             const int idx = lt + NL * u;
             const int r = idx / B8, c8 = (idx % B8) * 8;
-            offB[u] = (uint32_t)(((int64_t)(j0 + r) * K + c8) * 2);
+            offB[u] = (uint32_t)(((int64_t)r * K + c8) * 2);
             ldsB[u] = (uint32_t)(r * GSW + c8);
         }
         f4 ra[FDL][UA], rbh[FDL][UB], rbl[FDL][UB];
         auto fetch = [&](int slot, int kb) {
             const int k0 = min(kb, nk - 1) * GKT;
-            const char* const xk = reinterpret_cast<const char*>(X) + (size_t)k0 * 4;
-            const char* const hk = reinterpret_cast<const char*>(Whi) + (size_t)k0 * 2;
-            const char* const lk = reinterpret_cast<const char*>(Wlo) + (size_t)k0 * 2;
+            const char* const xk = xblk + (size_t)k0 * 4;
+            const char* const hk = hblk + (size_t)k0 * 2;
+            const char* const lk = lblk + (size_t)k0 * 2;
 #pragma unroll
             for (int u = 0; u < UA; ++u) ra[slot][u] = *reinterpret_cast<const f4*>(xk + offA[u]);
 #pragma unroll

@@ -719,6 +719,14 @@ struct ArgsB {
     float b_lin;
     int64_t wy_lo;  // offset (in f4) of the lo Wy image
     uint32_t info[kMaxWords];
+    // sweep / count mode (gru16p_kernel only): y, decoded and logits are nseg segments of (B, N) back to back; with
+    // counters != NULL the decision at position jj is compared with msg[cw][slot[jj]] (slot 255: not compared) and
+    // counters[2 s], [2 s + 1] += bit / block errors of segment s (npd_gru_decode_count_sweep)
+    const float* msg;
+    unsigned long long* counters;
+    int K;
+    int nseg;
+    uint32_t slotw[kMaxN / 4];  // byte jj & 3 of word jj >> 2 = slot of position jj (scalar-loaded per step)
 };
 
 __device__ __forceinline__ f16v mfma16(const bf8& a, const bf8& b, const f16v& c) {
@@ -1220,7 +1228,10 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
     const int col = lane & 15;
     const int N = a.N;
     const int nkb = N / 32;
-    const int64_t ntiles = (a.B + 15) / 16;
+    const int64_t tps = (a.B + 15) / 16;  // tiles per segment
+    const int64_t ntiles = tps * (a.nseg > 1 ? a.nseg : 1);
+    const bool count = a.counters != nullptr;
+    uint32_t be_w = 0, bl_w = 0;  // this wave's bit / block errors of the current segment (wave-uniform)
     // per-lane LDS byte bases, laundered so that every fragment / constant read is base + immediate offset
     uint32_t wbs[3];
 #pragma unroll
@@ -1240,14 +1251,33 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
 
     for (int64_t tile = (int64_t)blockIdx.x * NPD_GRU16_WPB + wave; tile < ntiles;
          tile += (int64_t)gridDim.x * NPD_GRU16_WPB) {
-        const int64_t cw = tile * 16 + col;
+        const int64_t seg = tile / tps;
+        const int64_t cw = (tile - seg * tps) * 16 + col;  // codeword within the segment
         const bool valid = cw < a.B;
         const int64_t cwc = valid ? cw : a.B - 1;
+        const int64_t rowoff = (seg * a.B + cw) * N;       // this codeword's row of y / decoded / logits
+        // count mode: the codeword's messages as 2-bit codes of rint(msg) (-1: 0, +1: 1, 0: 2, else 3; the decision
+        // d is in {-1, 0, +1}), slot sl held by row sl & 3 at bits 2 (q & 15) of word q >> 4, q = sl >> 2: 4 registers
+        // cover K <= 256, loaded once per tile, so no step waits on a message load
+        uint32_t mc[4] = {0u, 0u, 0u, 0u};
+        if (count) {
+            const float* mr = a.msg + cwc * a.K;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                for (int j = 0; j < 16; ++j) {
+                    const int sl = 4 * (16 * w + j) + g4;
+                    if (sl >= a.K) break;
+                    const float v = rintf(mr[sl]);
+                    const uint32_t code = v == -1.0f ? 0u : v == 1.0f ? 1u : v == 0.0f ? 2u : 3u;
+                    mc[w] |= code << (2 * j);
+                }
+        }
+        uint32_t nerr = 0;  // this row's share of the codeword's bit errors
         f4 P[G::RT];
 #pragma unroll
         for (int t = 0; t < G::RT; ++t) P[t] = c4(G::C0L0, t);
         if (a.y) {
-            const float* yr = a.y + cwc * N;
+            const float* yr = a.y + (seg * a.B + cwc) * N;
             for (int kb = 0; kb < nkb; ++kb) {
                 const f4 y0 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4);
                 const f4 y1 = *reinterpret_cast<const f4*>(yr + 32 * kb + 8 * g4 + 4);
@@ -1277,7 +1307,7 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
             h1[t] = zero;
         }
         if (a.h0) {  // register e of tile t = hidden unit 16 t + 4 g4 + e of codeword col (F = 64, 2 layers)
-            const float* hr = a.h0 + cwc * 128;
+            const float* hr = a.h0 + (seg * a.B + cwc) * 128;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1300,6 +1330,8 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
         for (int ii = 0; ii < N; ++ii) {
             const int jj = a.rev ? N - 1 - ii : ii;
             Upd4<SPLIT> u;
+            // count mode: this step's message slot (255: not compared), from the kernel arguments by a scalar load
+            const int sl = count ? (int)((a.slotw[jj >> 2] >> (8 * (jj & 3))) & 255u) : 255;
             // ================= layer 0
             f4 ap[3] = {a0[0] + fma4(xb, c4(G::C1L0, 0), P[0]), a0[1] + fma4(xb, c4(G::C1L0, 4), P[4]), a0[2]};
             f4 ainp = fma4(xb, c4(G::C1L0, 8), P[8]);
@@ -1367,10 +1399,16 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                     const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
                     float d;
                     if (info) d = out > 0.0f ? 1.0f : (out < 0.0f ? -1.0f : 0.0f);
-                    else d = a.gt ? a.gt[cwc * N + jj] : 1.0f;
+                    else d = a.gt ? a.gt[(seg * a.B + cwc) * N + jj] : 1.0f;
                     if (g4 == 0 && valid) {
-                        a.decoded[cw * N + jj] = d;
-                        if (a.logits) a.logits[cw * N + ii] = out;
+                        if (a.decoded) a.decoded[rowoff + jj] = d;
+                        if (a.logits) a.logits[rowoff + ii] = out;
+                    }
+                    if (sl != 255) {  // count_errors_kernel's test, rint(msg) != rint(d), on the 2-bit codes
+                        const int q = sl >> 2, w = q >> 4;
+                        const uint32_t mw = w == 0 ? mc[0] : w == 1 ? mc[1] : w == 2 ? mc[2] : mc[3];
+                        const uint32_t dc = d > 0.0f ? 1u : (d < 0.0f ? 0u : 2u);
+                        nerr += (g4 == (sl & 3) && ((mw >> (2 * (q & 15))) & 3u) != dc) ? 1u : 0u;
                     }
                     const float sd = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
                     xb = a.onehot ? (sd > 0.0f ? 1.0f : 0.0f) : sd;
@@ -1378,6 +1416,27 @@ __global__ __launch_bounds__(64 * NPD_GRU16_WPB) void gru16p_kernel(const ArgsB 
                     split_kb<SPLIT>(h1, c - 13, gh, gl);
                 }
             });
+        }
+        if (count) {
+            // the 16 codewords' errors: each row counted its slots; sum the four rows of every codeword
+            nerr += __shfl_xor(nerr, 16, 64);
+            nerr += __shfl_xor(nerr, 32, 64);
+            const bool mine = g4 == 0 && valid;
+            bl_w += (uint32_t)__builtin_popcountll(__ballot(mine && nerr != 0u));
+            uint32_t e = mine ? nerr : 0u;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) e += __shfl_xor(e, o, 64);
+            be_w += (uint32_t)__builtin_amdgcn_readfirstlane(e);
+            // flush when this wave's next tile is in another segment (or there is none): one atomic pair per
+            // wave and segment
+            const int64_t nt = tile + (int64_t)gridDim.x * NPD_GRU16_WPB;
+            if (nt >= ntiles || nt / tps != seg) {
+                if (lane == 0 && (be_w | bl_w)) {
+                    atomicAdd(a.counters + 2 * seg, (unsigned long long)be_w);
+                    atomicAdd(a.counters + 2 * seg + 1, (unsigned long long)bl_w);
+                }
+                be_w = bl_w = 0;
+            }
         }
     }
 }
@@ -1463,7 +1522,7 @@ static int launch16(const ArgsB& a, hipStream_t s) {
         NPD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
         attr = true;
     }
-    const int64_t tiles = (a.B + 15) / 16;
+    const int64_t tiles = (a.B + 15) / 16 * (a.nseg > 1 ? a.nseg : 1);
     const int64_t wgs = (tiles + NPD_GRU16_WPB - 1) / NPD_GRU16_WPB;
     const int grid = grid_for(wgs, 1, device_cu_count());
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NPD_GRU16_WPB), (size_t)Geo16::TOTAL * 4, s, a);
@@ -2094,6 +2153,7 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
         b.wy = reinterpret_cast<const gru::f4*>(g->wy);
         b.y = y; b.h0 = h0; b.gt = gt; b.decoded = decoded; b.logits = logits; b.B = B; b.N = g->N;
         b.rev = a.rev; b.onehot = a.onehot; b.b_lin = g->b_lin; b.wy_lo = g->wy_lo;
+        b.nseg = 1;
         for (int w = 0; w < kMaxWords; ++w) b.info[w] = a.info[w];
         if (g->img16) {
             b.img = g->img16;
@@ -2121,6 +2181,52 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
     if (g->F == 64) return gru::launch<64, 1>(a, s);
     if (g->layers == 2) return gru::launch<32, 2>(a, s);
     return gru::launch<32, 1>(a, s);
+}
+
+extern "C" int npd_gru_decode_count_sweep(const npd_gru* g, int n_seg, const float* y, const uint8_t* is_info,
+                                          int reverse, const float* msg, int K, const int32_t* cols, float* decoded,
+                                          int64_t B, unsigned long long* counters, void* stream) {
+    NPD_ARG(g != nullptr, "npd_gru_decode_count_sweep: gru is NULL");
+    NPD_ARG(B >= 0 && n_seg >= 0 && K >= 0, "npd_gru_decode_count_sweep: negative size");
+    if (B == 0 || n_seg == 0) return NPD_OK;
+    NPD_ARG(y != nullptr && is_info != nullptr && counters != nullptr && (K == 0 || (msg != nullptr && cols != nullptr)),
+            "npd_gru_decode_count_sweep: null pointer");
+    NPD_ARG(((uintptr_t)y & 15) == 0, "npd_gru_decode_count_sweep: y must be 16-byte aligned");
+    NPD_ARG(K <= g->N, "npd_gru_decode_count_sweep: K > N");
+    uint8_t slot[kMaxN];
+    memset(slot, 255, sizeof(slot));
+    for (int k = 0; k < K; ++k) {
+        NPD_ARG(cols[k] >= 0 && cols[k] < g->N, "npd_gru_decode_count_sweep: column out of range");
+        NPD_ARG(slot[cols[k]] == 255, "npd_gru_decode_count_sweep: repeated column");
+        slot[cols[k]] = (uint8_t)k;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (g->img16 == nullptr || g->cell != 0) {
+        // other kernels: one decode and one column count per segment (the same counts), into the caller's decoded
+        NPD_ARG(decoded != nullptr, "npd_gru_decode_count_sweep: handles other than the 16-codeword split kernel (F = 64, "
+                                    "2 layers, N % 32 == 0, precision != 0) need decoded (n_seg, B, N)");
+        const int64_t rows = B * g->N;
+        for (int sg = 0; sg < n_seg; ++sg) {
+            int rc = npd_gru_decode_ex(g, y + sg * rows, nullptr, is_info, reverse, nullptr, decoded + sg * rows, nullptr,
+                                       B, stream);
+            if (rc == NPD_OK && K > 0)
+                rc = npd_count_errors_cols(msg, decoded + sg * rows, B, K, g->N, cols, counters + 2 * sg, stream);
+            if (rc != NPD_OK) return rc;
+        }
+        return NPD_OK;
+    }
+    gru::ArgsB b{};
+    b.img = g->img16;
+    b.wy = reinterpret_cast<const gru::f4*>(g->wy16);
+    b.wy_lo = g->wy16_lo;
+    b.y = y; b.h0 = nullptr; b.gt = nullptr; b.decoded = decoded; b.logits = nullptr; b.B = B; b.N = g->N;
+    b.rev = reverse ? 1 : 0; b.onehot = g->onehot; b.b_lin = g->b_lin;
+    for (int w = 0; w < kMaxWords; ++w) b.info[w] = 0;
+    for (int i = 0; i < g->N; ++i)
+        if (is_info[i]) b.info[i >> 5] |= 1u << (i & 31);
+    b.msg = msg; b.counters = counters; b.K = K; b.nseg = n_seg;
+    memcpy(b.slotw, slot, sizeof(slot));
+    return g->split16 == 3 ? gru::launch16<3>(b, s) : g->split16 == 5 ? gru::launch16<5>(b, s) : gru::launch16<1>(b, s);
 }
 
 extern "C" int npd_gru_decode(const npd_gru* g, const float* y, const uint8_t* is_info, int reverse, const float* gt,

@@ -19,10 +19,14 @@ from . import _lib
 
 class RNN_Model(nn.Module):
     """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts nets with output_size 1,
-    out_linear_depth 1, unidirectional, no layernorm: GRU with decoding_type 'y_input' -- y_depth 0 (the CRISP
-    scripts, rnn_all.py:250-253) or --use_ynn's y-MLP of N outputs feeding the GRU in place of y (rnn_all.py:1319-1320,
-    :533-536) -- or 'y_h0' (the argparse default, rnn_all.py:73) with its y-MLP (y_linears, with or without skip); LSTM
-    (rnn_all.py:69) with 'y_input' or 'y_h0', fp32, hidden 32 or hidden 64 with one layer."""
+    out_linear_depth 1, no layernorm, 1 or 2 layers, GRU or LSTM cells (rnn_all.py:69) at hidden 32, 64, 128, 256 or
+    512 -- a bidirectional net (rnn_all.py:307) runs as the one-directional cell of hidden 2F, so its packed width 2F
+    must be one of those -- with decoding_type 'y_input' -- y_depth 0 (the CRISP scripts, rnn_all.py:250-253) or
+    --use_ynn's y-MLP of N outputs feeding the cell in place of y (rnn_all.py:1319-1320, :533-536) -- or 'y_h0' (the
+    argparse default, rnn_all.py:73) with its y-MLP (y_linears, with or without skip; LSTM: (h, c) both start from
+    it).  LSTM cells run fp32; the split precisions (fp16x3, bf16x3, bf16) cover GRUs of packed hidden <= 64, and
+    y_h0 in a split precision needs the 16-codeword kernel (hidden 64, 2 layers, N % 32 == 0).  fused_supported(...,
+    precision, N) mirrors these limits and npd_rnn_create's LDS bound for hidden 512 x 2 layers."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -101,10 +105,29 @@ class RNN_Model(nn.Module):
         decoded = self.linear(out if Fy is None else torch.cat([Fy, out], -1))
         return decoded.view(-1, self.output_size), hidden
 
-    def fused_supported(self, decoding_type="y_input") -> bool:
+    def fused_supported(self, decoding_type="y_input", precision="fp32", N=None) -> bool:
+        """True when npd_rnn_create / npd_gru_decode_ex accept this net for `decoding_type` at `precision` (and code
+        length N when given): the same limits, checked before any handle is built."""
         common = (self.output_size == 1 and self.out_linear_depth == 1
                   and isinstance(self.layernorm, nn.Identity) and self.num_rnn_layers in (1, 2))
         fe = self.feature_size * (2 if self.bidirectional else 1)  # a bidirectional net runs as the 2F cell
+        if N is not None:
+            # npd_gru_create: N a multiple of 8 in [8, 256]; the weight-streaming kernels hold both layers' states and
+            # the tile's y in LDS (gru::wide_lds_bytes), so hidden 512 x 2 layers needs N <= 128
+            nw = min(fe // 32, 8)
+            if not (8 <= N <= 256 and N % 8 == 0):
+                return False
+            if fe > 64 and (self.num_rnn_layers * fe * 32 + N * 32 + nw * 32) * 4 > 160 * 1024:
+                return False
+        if precision != "fp32":
+            # LSTM cells are fp32 only; the split kernels cover packed hidden <= 64 and need N % 16 == 0; an initial
+            # state (y_h0) in a split precision runs only on the 16-codeword kernel (hidden 64, 2 layers, N % 32 == 0)
+            if self.rnn_type == "LSTM" or fe > 64:
+                return False
+            if N is not None and N % 16:
+                return False
+            if decoding_type == "y_h0" and not (fe == 64 and self.num_rnn_layers == 2 and (N is None or N % 32 == 0)):
+                return False
         if self.rnn_type == "LSTM":  # fp32: lstm_decode_kernel (F 32, F 64 x 1 layer), lstm_wide_kernel (the rest)
             shape = fe in (32, 64, 128, 256, 512)
             if decoding_type == "y_h0":  # (h, c) both start from get_h0's x (rnn_all.py:370-375)
@@ -214,7 +237,7 @@ class RNN_decoder:
         if self.decoding_type not in ("y_input", "y_h0"):
             raise _lib.NpdError(f"fused decode supports decoding_type 'y_input' and 'y_h0', got {self.decoding_type!r}"
                                 " ('y_h0_out' builds a (1 + depth) F y-MLP that get_h0 cannot reshape, rnn_all.py:1324)")
-        if not (hasattr(net, "fused_supported") and net.fused_supported(self.decoding_type)):
+        if not (hasattr(net, "fused_supported") and net.fused_supported(self.decoding_type, self.precision, self.N)):
             raise _lib.NpdError("network configuration not supported by the fused GRU decoder")
         din = (self.N if self.decoding_type == "y_input" else 0) + 1 + int(self.onehot)
         if net.input_size != din:
@@ -239,6 +262,41 @@ class RNN_decoder:
                                                  _lib.ptr(logits), B, _lib.stream_of(y.device)), "npd_gru_decode")
         dec = _lib.home(dec, y_in)
         return (dec, _lib.home(logits, y_in)) if return_logits else dec
+
+    def decode_count_sweep(self, net, y, msg, counters, cols=None, decoded=None):
+        """The eval loop's GRU half over an SNR sweep (rnn_all.py:853-880): y (n_snr, B, N) on the GPU, msg (B, K) the
+        messages of the B codewords (every segment's), counters (n_snr, 2) += [bit errors, block errors] of
+        decode(net, False, y[s])[:, cols] against msg (cols defaults to the information set) -- npd_gru_decode_count_sweep:
+        ONE launch for the sweep on the 16-codeword split kernel (hidden 64, 2 layers, fp16x3 / bf16x3 / bf16), else a
+        decode + count per segment into `decoded` (n_snr, B, N), allocated here when not given.  y_input decoding."""
+        if self.decoding_type != "y_input" or net.y_depth > 0:
+            raise _lib.NpdError("decode_count_sweep covers y_input decoding without the y-MLP")
+        if not (hasattr(net, "fused_supported") and net.fused_supported("y_input", self.precision, self.N)):
+            raise _lib.NpdError("network configuration not supported by the fused GRU decoder")
+        _lib.require_gpu(y, "y")
+        if y.dim() != 3 or y.shape[2] != self.N:
+            raise ValueError(f"y must be (n_snr, B, {self.N}), got {tuple(y.shape)}")
+        n, B = y.shape[0], y.shape[1]
+        c = np.ascontiguousarray(np.asarray(self.info_inds if cols is None else cols, np.int64).reshape(-1), np.int32)
+        msg = _lib.f32c(_lib.stage(msg, "msg", y.device))
+        if msg.shape != (B, c.size):
+            raise ValueError(f"msg must be ({B}, {c.size}), got {tuple(msg.shape)}")
+        _lib.check_out(counters, "counters", torch.int64, 2 * n, y.device)
+        is_info = np.zeros(self.N, np.uint8)
+        is_info[np.asarray(self.info_inds, np.int64)] = 1
+        h = self._handle(net, y.device)
+        y = _lib.f32c(y)
+        fused = (self.precision != "fp32" and net.rnn_type == "GRU" and not net.bidirectional and net.feature_size == 64
+                 and net.num_rnn_layers == 2 and self.N % 32 == 0)
+        if decoded is None and not fused:
+            decoded = torch.empty(n, B, self.N, dtype=torch.float32, device=y.device)
+        _lib.check_out(decoded, "decoded", torch.float32, n * B * self.N, y.device, optional=True)
+        _lib.check(_lib.load().npd_gru_decode_count_sweep(h.h, n, _lib.ptr(y), is_info.ctypes.data_as(ctypes.c_void_p),
+                                                          1 if self.reverse_order else 0, _lib.ptr(msg), int(c.size),
+                                                          c.ctypes.data_as(ctypes.c_void_p), _lib.ptr(decoded), B,
+                                                          _lib.ptr(counters), _lib.stream_of(y.device)),
+                   "npd_gru_decode_count_sweep")
+        return counters
 
     def _h0(self, net, y):
         """(B, F * layers) initial states: get_h0's MLP (y first when the net was built with skip, rnn_all.py:369-370),

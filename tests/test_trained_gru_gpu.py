@@ -100,10 +100,15 @@ def fixture_code(d):
     return code, info
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
 @pytest.mark.parametrize("name", CASES)
-def test_trained_gru_ber_curve_matches_reference(name):
+def test_trained_gru_ber_curve_matches_reference(name, precision):
+    """fp32: the reference's arithmetic; fp16x3: the split path that carries the bench headline (gru16p_kernel<5>
+    at hidden 64 x 2 layers), held to the same z-tests and +-0.05 dB bar."""
     d = trained_fixture(name)
-    net, dec = build(d)
+    if precision != "fp32" and int(d["F"]) > 64:
+        pytest.skip("the split paths cover hidden <= 64; hidden 512 decodes on the fp32 gru_wide_kernel")
+    net, dec = build(d, precision)
     K = int(d["K"])
     code, info = fixture_code(d)
     snrs = [float(s) for s in d["snr"]]
