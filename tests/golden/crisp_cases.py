@@ -37,6 +37,12 @@ CASES = {
     "trained_crisp_64_32_h2e": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6432,
                                     curriculum=_cur(8, 5000, 32, 2000, 30000, 1000), ref_lr=2e-4,
                                     n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
+    # round 6: configs[2]'s code and width, Polar(64,32) hidden 64, on run_crisp.sh's full schedule --
+    # rev_polar (hard first), 10000 steps at K = 8, 5000 per K + 1 stage, 100000 at K = 32 (225k GPU steps, HIP-graph
+    # replayed steps), then the reference's rnn_all.py for the last stage
+    "trained_crisp_64_32_full": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6434,
+                                     curriculum=_cur(8, 10000, 32, 5000, 100000, 1000), ref_lr=2e-4,
+                                     n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
     # run_crisp.sh's own decoder: Polar(64,22), rate profile rev_polar (hard first), GRU hidden 512, 2 layers, onehot
     # y_input, K = 8 .. 22 with K + 1 per stage.  The script runs 10000 steps at K = 8, 5000 per later stage and 100000 at
     # K = 22 (175k steps); this case runs the same stage order on the GPU with shortened stages (a GPU-minute budget),

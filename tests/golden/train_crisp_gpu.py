@@ -146,6 +146,10 @@ def main():
                     help="bf16 autocast of the forward (training speed only; the fixture is whatever weights result, "
                          "and every parity claim rests on the reference's fp32 decoder run on them)")
     ap.add_argument("--probe", type=int, default=0, help="time this many steps and exit (no state written)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one whole training step (data, forward, backward, clip, AdamW) in a HIP graph and "
+                         "replay it: the hidden-64 step is launch-bound (~600 small kernels for the 64-step GRU and its "
+                         "backward); StepLR is applied by writing the tensor learning rate between replays")
     ap.add_argument("--init", default=None, help="weights ({'net': state_dict}) to start the first GPU stage from "
                                                   "(the reference-loop stages before the GPU block)")
     args = ap.parse_args()
@@ -194,7 +198,8 @@ def main():
         sigma = snr_db2sigma(c["snr_train"])
         net.train()
         t0, s0 = time.time(), st["step"]
-        for step in range(st["step"], steps):
+
+        def train_step():
             msg = 1 - 2 * (torch.rand(c["batch"], K, device=dev) < 0.5).float()
             gt = torch.ones(c["batch"], N, device=dev)
             gt[:, info_t] = msg
@@ -205,8 +210,42 @@ def main():
             loss.backward()
             torch.nn.utils.clip_grad_norm_(net.parameters(), 0.25)
             opt.step()
-            opt.zero_grad()
-            sched.step()
+            opt.zero_grad(set_to_none=not args.graph)
+            return loss
+
+        graph = None
+        if args.graph:
+            # capturable AdamW with a tensor learning rate (the same update rule); StepLR's value is written into it
+            lr_t = torch.tensor(sched.get_last_lr()[0], device=dev)
+            sd = opt.state_dict()
+            opt = torch.optim.AdamW(net.parameters(), lr=lr_t, capturable=True)
+            if st["step"] > 0 and "opt" in st:
+                sd["param_groups"][0]["lr"] = lr_t
+                sd["param_groups"][0]["capturable"] = True
+                opt.load_state_dict(sd)
+                for p_ in opt.state.values():
+                    if "step" in p_:
+                        p_["step"] = p_["step"].to(dev)
+                opt.param_groups[0]["lr"] = lr_t
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm-up outside the capture (allocations, AdamW state)
+                for _ in range(3):
+                    train_step()
+            torch.cuda.current_stream().wait_stream(side)  # (3 extra updates per resumed slice, kept)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                g_loss = train_step()
+        for step in range(st["step"], steps):
+            if graph is not None:
+                lr_now = c["lr"] * c["lr_gamma"] ** (step // c["lr_decay"])  # StepLR(lr_decay, gamma) before step
+                lr_t.fill_(lr_now)
+                graph.replay()
+                loss = g_loss
+                sched.step()
+            else:
+                loss = train_step()
+                sched.step()
             now = time.time()
             if args.probe and step + 1 - s0 == args.probe:
                 torch.cuda.synchronize()
