@@ -15,8 +15,10 @@
 // Activations of a chunk of codewords live in a caller-provided workspace, (B, N, C) (channels
 // contiguous); FC0's weights are permuted on the host to that flatten order.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <type_traits>
 #include <vector>
@@ -909,8 +911,12 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int GSW = 40;  // LDS row stride (halfs) of the 32-wide K blocks: 80 B, conflict-free ds_read_b128 rows
 constexpr int kWspSlots = 3;
 constexpr size_t kFcWspLds = (size_t)kWspSlots * 4 * FB * GSW * 2;
-template <int FDL>
-__global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Whi,
+// PRE: X arrives already split (fp16 hi / lo planes of X 2^SA, row-major like X, written by split_planes_kernel), so the
+// loaders only copy: 16-B loads of both planes into 16-B LDS stores, no split VALU
+template <int FDL, bool PRE>
+__global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Xhi,
+                                                              const uint16_t* __restrict__ Xlo,
+                                                              const uint16_t* __restrict__ Whi,
                                                               const uint16_t* __restrict__ Wlo,
                                                               const float* __restrict__ bias, float* __restrict__ out,
                                                               int M, int K, int Nout, int act, int sw,
@@ -919,8 +925,8 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
     constexpr int GKT = 32, NS = kWspSlots;
     static_assert(FDL >= 2 && FDL % NS == 0, "the prologue stashes two K blocks; LDS slots repeat with the ring");
     constexpr int NL = 256;                            // loader threads
-    constexpr int A4 = GKT / 4, B8 = GKT / 8;          // f4 per A row, 16-B pieces per B row
-    constexpr int UA = FB * A4 / NL, UB = FB * B8 / NL;  // 4, 2
+    constexpr int A4 = PRE ? GKT / 8 : GKT / 4, B8 = GKT / 8;  // 16-B pieces per A row (per plane), per B row
+    constexpr int UA = FB * A4 / NL, UB = FB * B8 / NL;  // 4 (fp32 X) or 2 per plane (PRE), 2
     constexpr int TM = 2, TN = 2;
     constexpr int PL = FB * GSW;  // halfs per plane
     const uint32_t am_raw = amax_in != nullptr ? __builtin_nontemporal_load(amax_in + (threadIdx.x & 63) * kAmaxStride) : 0u;
@@ -943,15 +949,17 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
         // per load, no 64-bit address arithmetic per K block.  The offsets are relative to the block's first row of X
         // and of W (64-bit bases), so they stay below 128 K 4 B < 2^28 at the largest accepted K = 512 x 1024
         const char* const xblk = reinterpret_cast<const char*>(X) + (size_t)m0 * K * 4;
+        const char* const xhblk = reinterpret_cast<const char*>(Xhi) + (size_t)m0 * K * 2;
+        const char* const xlblk = reinterpret_cast<const char*>(Xlo) + (size_t)m0 * K * 2;
         const char* const hblk = reinterpret_cast<const char*>(Whi) + (size_t)j0 * K * 2;
         const char* const lblk = reinterpret_cast<const char*>(Wlo) + (size_t)j0 * K * 2;
         uint32_t offA[UA], offB[UB], ldsA[UA], ldsB[UB];
 #pragma unroll
         for (int u = 0; u < UA; ++u) {
             const int idx = lt + NL * u;
-            const int r = idx / A4, c4 = (idx % A4) * 4;
+            const int r = idx / A4, c4 = (idx % A4) * (PRE ? 8 : 4);
             const int mr = min(m0 + r, M - 1) - m0;  // row within the block: < 128
-            offA[u] = (uint32_t)(((int64_t)mr * K + c4) * 4);
+            offA[u] = (uint32_t)(((int64_t)mr * K + c4) * (PRE ? 2 : 4));
             ldsA[u] = (uint32_t)(r * GSW + c4);
         }
 #pragma unroll
@@ -961,14 +969,22 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
             offB[u] = (uint32_t)(((int64_t)r * K + c8) * 2);
             ldsB[u] = (uint32_t)(r * GSW + c8);
         }
-        f4 ra[FDL][UA], rbh[FDL][UB], rbl[FDL][UB];
+        f4 ra[FDL][UA], ral[FDL][PRE ? UA : 1], rbh[FDL][UB], rbl[FDL][UB];
         auto fetch = [&](int slot, int kb) {
             const int k0 = min(kb, nk - 1) * GKT;
             const char* const xk = xblk + (size_t)k0 * 4;
             const char* const hk = hblk + (size_t)k0 * 2;
             const char* const lk = lblk + (size_t)k0 * 2;
+            if constexpr (PRE) {
 #pragma unroll
-            for (int u = 0; u < UA; ++u) ra[slot][u] = *reinterpret_cast<const f4*>(xk + offA[u]);
+                for (int u = 0; u < UA; ++u) {
+                    ra[slot][u] = *reinterpret_cast<const f4*>(xhblk + (size_t)k0 * 2 + offA[u]);
+                    ral[slot][u] = *reinterpret_cast<const f4*>(xlblk + (size_t)k0 * 2 + offA[u]);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < UA; ++u) ra[slot][u] = *reinterpret_cast<const f4*>(xk + offA[u]);
+            }
 #pragma unroll
             for (int u = 0; u < UB; ++u) {
                 rbh[slot][u] = *reinterpret_cast<const f4*>(hk + offB[u]);
@@ -977,6 +993,13 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
         };
         auto stash = [&](int slot, auto lds_slot) {
             _Float16* const base = smb + (size_t)decltype(lds_slot)::value * 4 * PL;
+            if constexpr (PRE) {
+#pragma unroll
+                for (int u = 0; u < UA; ++u) {
+                    *reinterpret_cast<f4*>(base + ldsA[u]) = ra[slot][u];
+                    *reinterpret_cast<f4*>(base + PL + ldsA[u]) = ral[slot][u];
+                }
+            } else
 #pragma unroll
             for (int u = 0; u < UA; ++u) {
                 hf4 hi, lo;
@@ -1096,7 +1119,29 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
     }
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
-#define FC_WSP fc_split_wsp_kernel<NPD_FC_FDL>
+#define FC_WSP fc_split_wsp_kernel<NPD_FC_FDL, false>
+#define FC_WSP_PRE fc_split_wsp_kernel<NPD_FC_FDL, true>
+
+// X (n floats, n % 4 == 0) -> fp16 planes hi = fp16(x 2^SA), lo = fp16(x 2^SA - hi), SA from the producer's max |x| as
+// in every split consumer (split_sa): the operands fc_split_wsp_kernel<.., true> copies instead of splitting
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ X, int64_t n4,
+                                                           const uint32_t* __restrict__ amax_in,
+                                                           uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+    const float sc = __builtin_ldexpf(1.0f, split_sa(amax_in));
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(X) + i);
+        hf4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = v[e] * sc;
+            h[e] = (_Float16)x;
+            l[e] = (_Float16)(x - (float)h[e]);
+        }
+        reinterpret_cast<hf4*>(hi)[i] = h;
+        reinterpret_cast<hf4*>(lo)[i] = l;
+    }
+}
 
 // ------------------------------------------------------------------------------ LayerNorm + sign
 __global__ __launch_bounds__(256) void layernorm_sign_kernel(const float* __restrict__ x, const float* __restrict__ g,
@@ -1340,6 +1385,11 @@ extern "C" int npd_conv_destroy(npd_conv* c) {
 }
 
 static int64_t chunk_of(int64_t B) { return B < kChunk ? B : kChunk; }
+// A/B switch NPD_FC0_PRESPLIT=0/1: FC0 on pre-split X planes (split_planes_kernel + fc_split_wsp_kernel<.., true>)
+static bool fc0_presplit() {
+    const char* e = getenv("NPD_FC0_PRESPLIT");
+    return e == nullptr || atoi(e) != 0;
+}
 // max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
 // record kLayers + f
 constexpr int kAmaxSlots = kLayers + 3;
@@ -1408,6 +1458,7 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
         const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
@@ -1532,6 +1583,8 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
             }
         }
         const float* flat = bufs[in_idx];  // (nb, N*E): l*E + c (FC0's weights are permuted to match)
+        int free_idx = 0;                   // an activation buffer no longer read: room for FC0's split planes
+        while (free_idx == in_idx) ++free_idx;
         const int64_t K1 = (int64_t)E * N;
         dim3 g1(4 * N / 64, (unsigned)((nb + 63) / 64));
         dim3 g2(N / 64, (unsigned)((nb + 63) / 64));
@@ -1544,10 +1597,23 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                 const uint16_t* wl = reinterpret_cast<const uint16_t*>(c->img + c->off_fc16[f][1]);
                 const uint32_t* am_in = amax + (f == 0 ? kLayers - 1 : kLayers + f - 1) * kAmaxWords;
                 uint32_t* am_out = f < 2 ? amax + (kLayers + f) * kAmaxWords : nullptr;  // FC2 feeds the fp32 LayerNorm
-                if (fo[f] % FB == 0) {
+                if (fo[f] % FB == 0 && f == 0 && fc0_presplit()) {
+                    // FC0's X split once into fp16 planes in a free activation buffer (layer 9's input: 4 B per
+                    // element, as X), then copied by the GEMM's loaders
+                    uint16_t* xh = reinterpret_cast<uint16_t*>(bufs[free_idx]);
+                    uint16_t* xl = xh + nb * K1;
+                    const int64_t n4 = nb * K1 / 4;
+                    const int gs = (int)std::min<int64_t>((n4 + 255) / 256, (int64_t)device_cu_count() * 8);
+                    hipLaunchKernelGGL(split_planes_kernel, dim3(gs), dim3(256), 0, s, flat, n4, am_in, xh, xl);
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    hipLaunchKernelGGL((FC_WSP), gb, dim3(512), kFcWspLds, s, fin[f], wh, wl, c->img + c->off_fc[f][1],
-                                       fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f], am_in, am_out);
+                    hipLaunchKernelGGL((FC_WSP_PRE), gb, dim3(512), kFcWspLds, s, fin[f], xh, xl, wh, wl,
+                                       c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
+                                       am_in, am_out);
+                } else if (fo[f] % FB == 0) {
+                    dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
+                    hipLaunchKernelGGL((FC_WSP), gb, dim3(512), kFcWspLds, s, fin[f], nullptr, nullptr, wh, wl,
+                                       c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
+                                       am_in, am_out);
                 } else {
                     hipLaunchKernelGGL(fc_split_kernel, f == 0 ? g1 : g2, dim3(256), 0, s, fin[f], wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
