@@ -1385,10 +1385,14 @@ extern "C" int npd_conv_destroy(npd_conv* c) {
 }
 
 static int64_t chunk_of(int64_t B) { return B < kChunk ? B : kChunk; }
-// A/B switch NPD_FC0_PRESPLIT=0/1: FC0 on pre-split X planes (split_planes_kernel + fc_split_wsp_kernel<.., true>)
+// A/B switch NPD_FC0_PRESPLIT=0/1 (default 0): FC0 on pre-split X planes (split_planes_kernel + fc_split_wsp_kernel<..,
+// true>).  Round 6 (profiles/round6/fc0_presplit_ab.txt): with copy-only loaders FC0 takes 935-938 us
+// per 4096 codewords against 1,061 us splitting in its loaders (-12 %), but the separate split pass costs 197 us, so the
+// default keeps the in-loader split; a split fused into the producing conv layer's epilogue would bound the gain at
+// those 12 % of FC0 (~3 % of the forward) -- the FC0 GEMM is not bound by its loaders' split work
 static bool fc0_presplit() {
     const char* e = getenv("NPD_FC0_PRESPLIT");
-    return e == nullptr || atoi(e) != 0;
+    return e != nullptr && atoi(e) != 0;
 }
 // max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
 // record kLayers + f
