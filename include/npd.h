@@ -238,6 +238,16 @@ int npd_gru_destroy(npd_gru* gru);
 int npd_rnn_create(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
                    npd_gru** out);
 /*
+ * npd_rnn_create with the reference's --use_layernorm head (rnn_all.py:317-320; forward rnn_all.py:387-398: decoded =
+ * linear(layernorm(out)), nn.LayerNorm(F) over the top layer's output): ln_weight / ln_bias (F, host) are its gamma /
+ * beta, ln_eps its eps.  The affine part folds into the output Linear (w gamma, b + w . beta); the kernel normalises each
+ * step's top-layer state (two-pass mean and biased variance over the F units).  GRU cells, fp32 (precision 0), F 32 or
+ * 64 (gru_decode_kernel), unidirectional (the reference's LayerNorm(F) does not take a bidirectional net's 2F output).
+ * ln_weight = NULL is npd_rnn_create.
+ */
+int npd_rnn_create_ex(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights,
+                      int precision, const float* ln_weight, const float* ln_bias, float ln_eps, npd_gru** out);
+/*
  * RNN_decoder.decode(net, False, y, gt) test branch (rnn_all.py:532-547): decoded (B,N) fp32, with
  * decoded[:, i] = sign(out_i) for i in the info set (is_info: N bytes, host) and 1 (or gt) else.
  * reverse: RNN_decoder reverse_order (rnn_all.py:414-416).  logits (B,N) optional: raw output at

@@ -35,6 +35,8 @@ struct npd_gru {
     int64_t wy16_lo;
     int split16;   // its SplitT variant
     int cell;      // 0 GRU, 1 LSTM (fp32)
+    int ln;        // use_layernorm head (rnn_all.py:317-320, :387-398): linear weights hold w * gamma, b_lin b + w . beta
+    float ln_eps;
 };
 
 namespace npd {
@@ -93,6 +95,8 @@ struct Args {
     int onehot;
     float b_lin;
     uint32_t info[kMaxWords];
+    int ln;                // LayerNorm head (gru_decode_kernel only)
+    float ln_eps;
 };
 
 __device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
@@ -308,7 +312,31 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                     part += wl * (L == 2 ? h1[t][i] : h0[t][i]);
                 }
             }
-            const float out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            float out;
+            if (a.ln) {
+                // LayerNorm head (rnn_all.py:387-398: linear(layernorm(out))): two-pass mean / biased variance over the
+                // F units of this codeword, then sum_i w_i gamma_i (h_i - mu) rstd + (b + w . beta) with the
+                // gamma-folded weights in the image (npd_rnn_create_ex)
+                float s1 = 0.0f;
+#pragma unroll
+                for (int t = 0; t < HT; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) s1 += L == 2 ? h1[t][i] : h0[t][i];
+                const float mu = (s1 + __shfl_xor(s1, 32, 64)) * (1.0f / (float)F);
+                float s2 = 0.0f, pw = 0.0f;
+#pragma unroll
+                for (int t = 0; t < HT; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const float d = (L == 2 ? h1[t][i] : h0[t][i]) - mu;
+                        s2 = fmaf(d, d, s2);
+                        pw = fmaf(smem[G::OFF_WL + (half * HT + t) * 16 + i], d, pw);
+                    }
+                const float var = (s2 + __shfl_xor(s2, 32, 64)) * (1.0f / (float)F);
+                out = (pw + __shfl_xor(pw, 32, 64)) / sqrtf(var + a.ln_eps) + a.b_lin;
+            } else {
+                out = part + __shfl_xor(part, 32, 64) + a.b_lin;
+            }
             const bool info = (a.info[jj >> 5] >> (jj & 31)) & 1u;
             float d;
             if (info) {
@@ -2018,6 +2046,32 @@ extern "C" int npd_rnn_create(int cell, int N, int F, int layers, int onehot, co
     return create_lstm(N, F, layers, onehot, weights, n_weights, precision, out);
 }
 
+extern "C" int npd_rnn_create_ex(int cell, int N, int F, int layers, int onehot, const float* weights,
+                                 int64_t n_weights, int precision, const float* ln_weight, const float* ln_bias,
+                                 float ln_eps, npd_gru** out) {
+    if (ln_weight == nullptr) return npd_rnn_create(cell, N, F, layers, onehot, weights, n_weights, precision, out);
+    NPD_ARG(out != nullptr, "npd_rnn_create_ex: out is NULL");
+    *out = nullptr;
+    NPD_ARG(weights != nullptr && ln_bias != nullptr, "npd_rnn_create_ex: null pointer");
+    NPD_ARG(cell == 0 && precision == 0 && (F == 32 || F == 64),
+            "npd_rnn_create_ex: the LayerNorm head runs on the fp32 GRU kernel (cell 0, precision 0, F 32 or 64)");
+    NPD_ARG(n_weights > F, "npd_rnn_create_ex: weight count too small");
+    // fold the LayerNorm's affine part into the output Linear: w' = w gamma, b' = b + sum w beta (in order, fp32)
+    std::vector<float> w(weights, weights + n_weights);
+    float* wl = w.data() + n_weights - F - 1;
+    float bsum = w[n_weights - 1];
+    for (int i = 0; i < F; ++i) {
+        bsum += wl[i] * ln_bias[i];
+        wl[i] *= ln_weight[i];
+    }
+    w[n_weights - 1] = bsum;
+    const int rc = npd_gru_create(N, F, layers, onehot, w.data(), n_weights, 0, out);
+    if (rc != NPD_OK) return rc;
+    (*out)->ln = 1;
+    (*out)->ln_eps = ln_eps;
+    return NPD_OK;
+}
+
 extern "C" int npd_gru_create(int N, int F, int layers, int onehot, const float* weights, int64_t n_weights,
                               int precision, npd_gru** out) {
     NPD_ARG(out != nullptr, "npd_gru_create: out is NULL");
@@ -2135,6 +2189,8 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
     a.rev = reverse ? 1 : 0;
     a.onehot = g->onehot;
     a.b_lin = g->b_lin;
+    a.ln = g->ln;
+    a.ln_eps = g->ln_eps;
     for (int w = 0; w < kMaxWords; ++w) a.info[w] = 0;
     for (int i = 0; i < g->N; ++i)
         if (is_info[i]) a.info[i >> 5] |= 1u << (i & 31);

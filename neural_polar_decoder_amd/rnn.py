@@ -19,14 +19,16 @@ from . import _lib
 
 class RNN_Model(nn.Module):
     """Same parameters as the reference (rnn_all.py:294-385).  The fused decoder accepts nets with output_size 1,
-    out_linear_depth 1, no layernorm, 1 or 2 layers, GRU or LSTM cells (rnn_all.py:69) at hidden 32, 64, 128, 256 or
+    out_linear_depth 1, 1 or 2 layers, GRU or LSTM cells (rnn_all.py:69) at hidden 32, 64, 128, 256 or
     512 -- a bidirectional net (rnn_all.py:307) runs as the one-directional cell of hidden 2F, so its packed width 2F
     must be one of those -- with decoding_type 'y_input' -- y_depth 0 (the CRISP scripts, rnn_all.py:250-253) or
     --use_ynn's y-MLP of N outputs feeding the cell in place of y (rnn_all.py:1319-1320, :533-536) -- or 'y_h0' (the
     argparse default, rnn_all.py:73) with its y-MLP (y_linears, with or without skip; LSTM: (h, c) both start from
     it).  LSTM cells run fp32; the split precisions (fp16x3, bf16x3, bf16) cover GRUs of packed hidden <= 64, and
     y_h0 in a split precision needs the 16-codeword kernel (hidden 64, 2 layers, N % 32 == 0).  fused_supported(...,
-    precision, N) mirrors these limits and npd_rnn_create's LDS bound for hidden 512 x 2 layers."""
+    precision, N) mirrors these limits and npd_rnn_create's LDS bound for hidden 512 x 2 layers.  --use_layernorm nets
+    (LayerNorm(F) before the output Linear, rnn_all.py:317-320, :387-398) run on the fp32 GRU kernel at hidden 32 / 64
+    (npd_rnn_create_ex); out_linear_depth > 1 heads are not fused."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -108,9 +110,12 @@ class RNN_Model(nn.Module):
     def fused_supported(self, decoding_type="y_input", precision="fp32", N=None) -> bool:
         """True when npd_rnn_create / npd_gru_decode_ex accept this net for `decoding_type` at `precision` (and code
         length N when given): the same limits, checked before any handle is built."""
-        common = (self.output_size == 1 and self.out_linear_depth == 1
-                  and isinstance(self.layernorm, nn.Identity) and self.num_rnn_layers in (1, 2))
         fe = self.feature_size * (2 if self.bidirectional else 1)  # a bidirectional net runs as the 2F cell
+        # LayerNorm head: the fp32 GRU kernel (npd_rnn_create_ex), hidden 32 / 64, unidirectional
+        ln_ok = isinstance(self.layernorm, nn.Identity) or (
+            isinstance(self.layernorm, nn.LayerNorm) and self.rnn_type == "GRU" and not self.bidirectional
+            and fe in (32, 64) and precision == "fp32")
+        common = self.output_size == 1 and self.out_linear_depth == 1 and ln_ok and self.num_rnn_layers in (1, 2)
         if N is not None:
             # npd_gru_create: N a multiple of 8 in [8, 256]; the weight-streaming kernels hold both layers' states and
             # the tile's y in LDS (gru::wide_lds_bytes), so hidden 512 x 2 layers needs N <= 128
@@ -176,12 +181,19 @@ def pack_gru_weights(net: nn.Module, layers: int, y_cols: int = 0) -> np.ndarray
 
 
 class _GruHandle:
-    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0, cell=0):
+    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0, cell=0, ln=None):
         L = _lib.load()
         out = ctypes.c_void_p()
-        _lib.check(L.npd_rnn_create(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
-                                    W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision), ctypes.byref(out)),
-                   "npd_rnn_create")
+        if ln is None:
+            _lib.check(L.npd_rnn_create(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
+                                        W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision),
+                                        ctypes.byref(out)), "npd_rnn_create")
+        else:  # (gamma, beta, eps) of the --use_layernorm head
+            g, b, eps = ln
+            _lib.check(L.npd_rnn_create_ex(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
+                                           W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision),
+                                           g.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p),
+                                           float(eps), ctypes.byref(out)), "npd_rnn_create_ex")
         self.h = out
 
     def __del__(self):
@@ -224,9 +236,13 @@ class RNN_decoder:
         if h is None:
             self._cache.clear()
             W = pack_gru_weights(net, net.num_rnn_layers, self.N if self.decoding_type == "y_h0" else 0)
+            ln = None
+            if isinstance(net.layernorm, nn.LayerNorm):
+                ln = (np.ascontiguousarray(net.layernorm.weight.detach().float().cpu().numpy()),
+                      np.ascontiguousarray(net.layernorm.bias.detach().float().cpu().numpy()), net.layernorm.eps)
             with torch.cuda.device(device):
                 h = _GruHandle(self.N, net.feature_size * (2 if net.bidirectional else 1), net.num_rnn_layers, self.onehot, W,
-                               self.PRECISIONS[self.precision], 1 if net.rnn_type == "LSTM" else 0)
+                               self.PRECISIONS[self.precision], 1 if net.rnn_type == "LSTM" else 0, ln)
             self._cache[key] = h
         return h
 

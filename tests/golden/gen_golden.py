@@ -510,6 +510,44 @@ def gen_gru_yh0_skip():
              **{"w." + k: v for k, v in sd.items()})
 
 
+def gen_gru_ln():
+    """--use_layernorm nets (rnn_all.py:317-320: nn.LayerNorm(F) on the RNN output before the output Linear, forward
+    rnn_all.py:387-398): y_input (Polar(32,16), hidden 64, 2 layers, one-hot; Polar(16,8), hidden 32, 1 layer, sign input,
+    reverse order) and y_h0 (Polar(32,16), hidden 32, 2 layers, selu y-MLP).  The LayerNorm's gamma / beta are drawn
+    away from their (1, 0) initialisation so the affine part is exercised; logits from a forward hook on net.linear."""
+    cases = [("gru_ln_polar_32_16", "y_input", 32, 16, 64, 2, True, False, "selu", 0, 0, 320, 4001),
+             ("gru_ln_polar_16_8_l1_noonehot_rev", "y_input", 16, 8, 32, 1, False, True, "selu", 0, 0, 256, 4002),
+             ("gru_ln_yh0_polar_32_16_f32", "y_h0", 32, 16, 32, 2, True, False, "selu", 64, 2, 256, 4003)]
+    for name, dtype, N, K, F, L, onehot, rev, act, yh, yd, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        din = (N if dtype == "y_input" else 0) + 1 + int(onehot)
+        net = rnn_m.RNN_Model("GRU", din, F, 1, L, N, yh, yd, act, 0.0, False, use_layernorm=True)
+        with torch.no_grad():
+            net.layernorm.weight.copy_(1.0 + 0.4 * torch.randn(F))
+            net.layernorm.bias.copy_(0.2 * torch.randn(F))
+        net.eval()
+        dec = rnn_m.RNN_decoder(dtype, N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits = [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, layers=L, onehot=int(onehot), rev=int(rev),
+             decoding_type=np.bytes_(dtype), activation=np.bytes_(act), y_hidden=yh, y_depth=yd,
+             ln_eps=np.float64(net.layernorm.eps), **{"w." + k: v for k, v in sd.items()})
+
+
 def gen_gru_ynn():
     """decoding_type 'y_input' with --use_ynn (rnn_all.py:1319-1320: y_output_size = N, the y-MLP's output replaces y as
     the GRU input; decode test branch rnn_all.py:533-536 Fy = net.get_Fy(y), then the y_input loop on [Fy, onehot]):
@@ -693,6 +731,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "lstm", "lstm_yh0", "rnn_bi", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "gru_ln", "lstm", "lstm_yh0", "rnn_bi", "conv"]
     for w in which:
         globals()["gen_" + w]()
