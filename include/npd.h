@@ -238,15 +238,21 @@ int npd_gru_destroy(npd_gru* gru);
 int npd_rnn_create(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights, int precision,
                    npd_gru** out);
 /*
- * npd_rnn_create with the reference's --use_layernorm head (rnn_all.py:317-320; forward rnn_all.py:387-398: decoded =
- * linear(layernorm(out)), nn.LayerNorm(F) over the top layer's output): ln_weight / ln_bias (F, host) are its gamma /
- * beta, ln_eps its eps.  The affine part folds into the output Linear (w gamma, b + w . beta); the kernel normalises each
- * step's top-layer state (two-pass mean and biased variance over the F units).  GRU cells, fp32 (precision 0), F 32 or
- * 64 (gru_decode_kernel), unidirectional (the reference's LayerNorm(F) does not take a bidirectional net's 2F output).
- * ln_weight = NULL is npd_rnn_create.
+ * npd_rnn_create with the reference's other output heads (rnn_all.py:317-343; forward rnn_all.py:387-398: decoded =
+ * linear(layernorm(out))).  GRU cells, fp32 (precision 0), F 32 or 64 (gru_decode_kernel), unidirectional.
+ *  - --use_layernorm: ln_weight / ln_bias (F, host) are nn.LayerNorm(F)'s gamma / beta, ln_eps its eps.  The affine part
+ *    folds into the output Linear (w gamma, b + w . beta); the kernel normalises each step's top-layer state (two-pass
+ *    mean and biased variance over the F units).  ln_weight = NULL: no LayerNorm.
+ *  - --out_linear_depth > 1 (head_depth): linear = Linear(F, H), SELU, [Linear(H, H), SELU] x (depth - 2), Linear(H, 1)
+ *    with H = head_hidden (the net's y_hidden_size, 1 .. 128); head_weights (host) = the Linear layers' weight and
+ *    bias in order (W_0 (H, F), b_0 (H), ..., W_last (1, H), b_last (1)), n_head values; the last F + 1 values of
+ *    `weights` (the depth-1 linear) are then ignored.  Each head layer is an fp32 MFMA GEMM per step inside the decode
+ *    loop.  head_depth = 1: the plain Linear(F, 1) of `weights`.  Not combined with the LayerNorm.
+ * ln_weight = NULL and head_depth = 1 is npd_rnn_create.
  */
 int npd_rnn_create_ex(int cell, int N, int F, int layers, int onehot, const float* weights, int64_t n_weights,
-                      int precision, const float* ln_weight, const float* ln_bias, float ln_eps, npd_gru** out);
+                      int precision, const float* ln_weight, const float* ln_bias, float ln_eps, int head_depth,
+                      int head_hidden, const float* head_weights, int64_t n_head, npd_gru** out);
 /*
  * RNN_decoder.decode(net, False, y, gt) test branch (rnn_all.py:532-547): decoded (B,N) fp32, with
  * decoded[:, i] = sign(out_i) for i in the info set (is_info: N bytes, host) and 1 (or gt) else.

@@ -55,7 +55,7 @@ SIGNATURES = [
     ("npd_gru_decode", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     ("npd_rnn_create", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, ctypes.POINTER(c_void_p)]),
     ("npd_rnn_create_ex", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_i64, c_int, c_void_p, c_void_p,
-                                  c_float, ctypes.POINTER(c_void_p)]),
+                                  c_float, c_int, c_int, c_void_p, c_i64, ctypes.POINTER(c_void_p)]),
     ("npd_gru_decode_ex", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64,
                                   c_void_p]),
     ("npd_gru_decode_count_sweep", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,

@@ -37,6 +37,9 @@ struct npd_gru {
     int cell;      // 0 GRU, 1 LSTM (fp32)
     int ln;        // use_layernorm head (rnn_all.py:317-320, :387-398): linear weights hold w * gamma, b_lin b + w . beta
     float ln_eps;
+    float* hd;     // out_linear_depth > 1 head image (device; head_image below), or NULL
+    int hd_depth, hd_tiles;
+    float hd_bout;
 };
 
 namespace npd {
@@ -97,6 +100,9 @@ struct Args {
     uint32_t info[kMaxWords];
     int ln;                // LayerNorm head (gru_decode_kernel only)
     float ln_eps;
+    const f4* hd;          // out_linear_depth > 1 head (gru_decode_kernel<.., HDT > 0>): image, depth, last bias
+    int hd_depth;
+    float hd_bout;
 };
 
 __device__ __forceinline__ f16v mfma(float a, float b, const f16v& c) {
@@ -148,6 +154,44 @@ __device__ __forceinline__ f2v rcp_2(f2v x) { return f2v{__builtin_amdgcn_rcpf(x
 
 // FOLD: the image's gate rows were pre-multiplied by their exp2 constants (build_image(..., fold)): the accumulators
 // already hold -log2(e) a (r, z) and -2 log2(e) a (n), so no scaling multiply per gate
+// gemm_chain with the A operands in global memory (the out_linear_depth > 1 head's image: a few KB, the same for every
+// wave, so they come from L1 / L2), one group of 4 k-steps ahead of the MFMAs
+template <int KG, int NT, int HT>
+__device__ __forceinline__ void gemm_chain_g(const f4* __restrict__ W, int lane, f16v (&acc)[NT], const f16v (&h)[HT]) {
+    f4 wc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wc[t] = W[(t * KG) * 64 + lane];
+#pragma unroll
+    for (int s4 = 0; s4 < KG; ++s4) {
+        f4 wn[NT];
+        if (s4 + 1 < KG) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) wn[t] = W[(t * KG + s4 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int s = 4 * s4 + e;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma(wc[t][e], h[s >> 4][s & 15], acc[t]);
+        }
+        if (s4 + 1 < KG) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) wc[t] = wn[t];
+        }
+    }
+}
+
+// nn.SELU (the out_linear_depth > 1 head's activation, rnn_all.py:336-343)
+__device__ __forceinline__ float selu(float x) {
+    return 1.0507009873554805f * (x > 0.0f ? x : 1.6732632423543772f * expm1f(x));
+}
+
+// head image (floats): per hidden layer l = 0 .. depth - 2: A operands [HDT tiles][K_l / 8 groups][64 lanes][4] (K_0 = F,
+// else 32 HDT), then its bias in accumulator order [HDT][2 halves][16]; then the last Linear's weights [2][HDT][16]
+__host__ __device__ inline int head_layer_off(int l, int F, int hdt) {
+    return l == 0 ? 0 : hdt * (F / 8) * 256 + hdt * 32 + (l - 1) * (hdt * (4 * hdt) * 256 + hdt * 32);
+}
+
 template <bool FOLD = false>
 __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& az, const f16v& ain, const f16v& ahn) {
     const f2v one = {1.0f, 1.0f};
@@ -186,7 +230,7 @@ __device__ __forceinline__ void gru_update(f16v& h, const f16v& ar, const f16v& 
 // The image's gate rows carry their exp2 constants (build_image(..., fold = true)) and the biases initialise the
 // accumulators (Geo::OFF_CV): only layer 0's r, z tiles keep the [1, x_i] k-step.  Measured in round 3 (same box,
 // alternating, 2^20 Polar(64,32) words): folding 41.0 -> 40.3 ms, bias initialisation 40.07 -> 39.70 ms.
-template <int F, int L, int WPB = NPD_GRU_WPB>
+template <int F, int L, int WPB = NPD_GRU_WPB, int HDT = 0>
 __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
     constexpr bool FOLD = true, BINIT = true;
     using G = Geo<F, L>;
@@ -313,7 +357,46 @@ __global__ __launch_bounds__(64 * WPB) void gru_decode_kernel(const Args a) {
                 }
             }
             float out;
-            if (a.ln) {
+            if constexpr (HDT > 0) {
+                // out_linear_depth > 1 head (rnn_all.py:336-343: Linear(F, H), SELU, [Linear(H, H), SELU] ..., Linear(H, 1)),
+                // H padded to 32 HDT with zero rows / columns: each layer is a GEMM whose accumulator tiles are,
+                // register for register, the next layer's B operand (as the GRU states are)
+                const float* hdf = reinterpret_cast<const float*>(a.hd);
+                f16v hx[HDT];
+                auto bias_init = [&](int l, f16v (&acc)[HDT]) {
+                    const int boff = head_layer_off(l, F, HDT) + HDT * (l == 0 ? F / 8 : 4 * HDT) * 256;
+#pragma unroll
+                    for (int t = 0; t < HDT; ++t) {
+                        const f4* p = reinterpret_cast<const f4*>(hdf + boff + (t * 2 + half) * 16);
+                        const f4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+                        acc[t] = f16v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3],
+                                      x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+                    }
+                };
+                bias_init(0, hx);
+                if constexpr (L == 2) gemm_chain_g<F / 8, HDT, HT>(a.hd, lane, hx, h1);
+                else gemm_chain_g<F / 8, HDT, HT>(a.hd, lane, hx, h0);
+#pragma unroll
+                for (int t = 0; t < HDT; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) hx[t][i] = selu(hx[t][i]);
+                for (int l = 1; l < a.hd_depth - 1; ++l) {
+                    f16v hn[HDT];
+                    bias_init(l, hn);
+                    gemm_chain_g<4 * HDT, HDT, HDT>(a.hd + head_layer_off(l, F, HDT) / 4, lane, hn, hx);
+#pragma unroll
+                    for (int t = 0; t < HDT; ++t)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) hx[t][i] = selu(hn[t][i]);
+                }
+                const float* wo = hdf + head_layer_off(a.hd_depth - 1, F, HDT);
+                float po = 0.0f;
+#pragma unroll
+                for (int t = 0; t < HDT; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) po = fmaf(wo[(half * HDT + t) * 16 + i], hx[t][i], po);
+                out = po + __shfl_xor(po, 32, 64) + a.hd_bout;
+            } else if (a.ln) {
                 // LayerNorm head (rnn_all.py:387-398: linear(layernorm(out))): two-pass mean / biased variance over the
                 // F units of this codeword, then sum_i w_i gamma_i (h_i - mu) rstd + (b + w . beta) with the
                 // gamma-folded weights in the image (npd_rnn_create_ex)
@@ -454,11 +537,47 @@ static void build_image(const float* W, int N, int onehot, std::vector<float>& i
             }
 }
 
-template <int F, int L>
+// the out_linear_depth > 1 head's image (layout: head_layer_off): hw = the Sequential's Linear layers in order, W_0 (H, F),
+// b_0 (H), [W_l (H, H), b_l (H)] for l = 1 .. depth - 2, W_last (1, H), b_last (1); H padded to 32 hdt with zeros
+static void build_head_image(const float* hw, int F, int H, int depth, int hdt, std::vector<float>& img, float& bout) {
+    const int HP = 32 * hdt;
+    img.assign((size_t)head_layer_off(depth - 1, F, hdt) + 2 * hdt * 16, 0.0f);
+    const float* p = hw;
+    for (int l = 0; l < depth - 1; ++l) {
+        const int K = l == 0 ? F : H, KP = l == 0 ? F : HP, KG = KP / 8;
+        const float* W = p;
+        const float* b = p + (size_t)H * K;
+        p = b + H;
+        float* im = img.data() + head_layer_off(l, F, hdt);
+        for (int t = 0; t < hdt; ++t)
+            for (int s = 0; s < KP / 2; ++s)
+                for (int ln = 0; ln < 64; ++ln) {
+                    const int row = 32 * t + (ln & 31), k = hid_of(s, ln >> 5);
+                    im[((size_t)(t * KG + s / 4) * 64 + ln) * 4 + (s & 3)] = row < H && k < K ? W[(size_t)row * K + k] : 0.0f;
+                }
+        float* bv = im + (size_t)hdt * KG * 256;
+        for (int t = 0; t < hdt; ++t)
+            for (int hf = 0; hf < 2; ++hf)
+                for (int i = 0; i < 16; ++i) {
+                    const int row = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hf;
+                    bv[(t * 2 + hf) * 16 + i] = row < H ? b[row] : 0.0f;
+                }
+    }
+    float* wo = img.data() + head_layer_off(depth - 1, F, hdt);
+    for (int hf = 0; hf < 2; ++hf)
+        for (int t = 0; t < hdt; ++t)
+            for (int i = 0; i < 16; ++i) {
+                const int k = hid_of(16 * t + i, hf);
+                wo[(hf * hdt + t) * 16 + i] = k < H ? p[k] : 0.0f;
+            }
+    bout = p[H];
+}
+
+template <int F, int L, int HDT = 0>
 static int launch(const Args& a, hipStream_t s) {
     using G = Geo<F, L>;
     constexpr int WPB = NPD_GRU_WPB;
-    auto kern = gru_decode_kernel<F, L, WPB>;
+    auto kern = gru_decode_kernel<F, L, WPB, HDT>;
     const size_t lds = (size_t)G::TOTAL * 4;
     static bool attr = false;
     if (!attr) {
@@ -2046,12 +2165,46 @@ extern "C" int npd_rnn_create(int cell, int N, int F, int layers, int onehot, co
     return create_lstm(N, F, layers, onehot, weights, n_weights, precision, out);
 }
 
+static int attach_head(npd_gru* g, int F, int head_depth, int head_hidden, const float* head_weights, int64_t n_head) {
+    const int H = head_hidden;
+    int64_t expect = (int64_t)H * F + H + (int64_t)(head_depth - 2) * (H * H + H) + H + 1;
+    NPD_ARG(n_head == expect, "npd_rnn_create_ex: head weight count does not match (F, head_depth, head_hidden)");
+    const int hdt = H <= 32 ? 1 : H <= 64 ? 2 : 4;
+    std::vector<float> img;
+    float bout = 0.0f;
+    gru::build_head_image(head_weights, F, H, head_depth, hdt, img, bout);
+    hipError_t e = hipMalloc(&g->hd, img.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(g->hd, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "npd_rnn_create_ex (head)");
+    g->hd_depth = head_depth;
+    g->hd_tiles = hdt;
+    g->hd_bout = bout;
+    return NPD_OK;
+}
+
 extern "C" int npd_rnn_create_ex(int cell, int N, int F, int layers, int onehot, const float* weights,
                                  int64_t n_weights, int precision, const float* ln_weight, const float* ln_bias,
-                                 float ln_eps, npd_gru** out) {
-    if (ln_weight == nullptr) return npd_rnn_create(cell, N, F, layers, onehot, weights, n_weights, precision, out);
+                                 float ln_eps, int head_depth, int head_hidden, const float* head_weights,
+                                 int64_t n_head, npd_gru** out) {
     NPD_ARG(out != nullptr, "npd_rnn_create_ex: out is NULL");
     *out = nullptr;
+    NPD_ARG(head_depth == 1 || (head_depth >= 2 && head_depth <= 8), "npd_rnn_create_ex: head_depth must be 1 .. 8");
+    if (head_depth > 1) {
+        NPD_ARG(head_weights != nullptr && weights != nullptr, "npd_rnn_create_ex: null pointer");
+        NPD_ARG(ln_weight == nullptr, "npd_rnn_create_ex: a LayerNorm before an out_linear_depth > 1 head is not fused");
+        NPD_ARG(cell == 0 && precision == 0 && (F == 32 || F == 64) && head_hidden >= 1 && head_hidden <= 128,
+                "npd_rnn_create_ex: the out_linear_depth > 1 head runs on the fp32 GRU kernel (cell 0, precision 0, "
+                "F 32 or 64, head_hidden 1 .. 128)");
+        int rc = npd_gru_create(N, F, layers, onehot, weights, n_weights, 0, out);
+        if (rc != NPD_OK) return rc;
+        rc = attach_head(*out, F, head_depth, head_hidden, head_weights, n_head);
+        if (rc != NPD_OK) {
+            npd_gru_destroy(*out);
+            *out = nullptr;
+        }
+        return rc;
+    }
+    if (ln_weight == nullptr) return npd_rnn_create(cell, N, F, layers, onehot, weights, n_weights, precision, out);
     NPD_ARG(weights != nullptr && ln_bias != nullptr, "npd_rnn_create_ex: null pointer");
     NPD_ARG(cell == 0 && precision == 0 && (F == 32 || F == 64),
             "npd_rnn_create_ex: the LayerNorm head runs on the fp32 GRU kernel (cell 0, precision 0, F 32 or 64)");
@@ -2157,6 +2310,7 @@ extern "C" int npd_gru_destroy(npd_gru* g) {
     if (g->wy) (void)hipFree(g->wy);
     if (g->img16) (void)hipFree(g->img16);
     if (g->wy16) (void)hipFree(g->wy16);
+    if (g->hd) (void)hipFree(g->hd);
     delete g;
     return NPD_OK;
 }
@@ -2191,6 +2345,9 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
     a.b_lin = g->b_lin;
     a.ln = g->ln;
     a.ln_eps = g->ln_eps;
+    a.hd = reinterpret_cast<const gru::f4*>(g->hd);
+    a.hd_depth = g->hd_depth;
+    a.hd_bout = g->hd_bout;
     for (int w = 0; w < kMaxWords; ++w) a.info[w] = 0;
     for (int i = 0; i < g->N; ++i)
         if (is_info[i]) a.info[i >> 5] |= 1u << (i & 31);
@@ -2232,6 +2389,16 @@ extern "C" int npd_gru_decode_ex(const npd_gru* g, const float* y, const float* 
         if (g->F == 512) return g->layers == 2 ? gru::launch_wide<512, 2>(a, g->N, s) : gru::launch_wide<512, 1>(a, g->N, s);
         if (g->F == 256) return g->layers == 2 ? gru::launch_wide<256, 2>(a, g->N, s) : gru::launch_wide<256, 1>(a, g->N, s);
         return g->layers == 2 ? gru::launch_wide<128, 2>(a, g->N, s) : gru::launch_wide<128, 1>(a, g->N, s);
+    }
+    if (g->hd != nullptr) {  // out_linear_depth > 1 head (npd_rnn_create_ex): 1, 2 or 4 tiles of 32 head units
+#define NPD_LHD(FF, LL) \
+        return g->hd_tiles == 1 ? gru::launch<FF, LL, 1>(a, s) : g->hd_tiles == 2 ? gru::launch<FF, LL, 2>(a, s) \
+                                                                                   : gru::launch<FF, LL, 4>(a, s)
+        if (g->F == 64 && g->layers == 2) NPD_LHD(64, 2);
+        if (g->F == 64) NPD_LHD(64, 1);
+        if (g->layers == 2) NPD_LHD(32, 2);
+        NPD_LHD(32, 1);
+#undef NPD_LHD
     }
     if (g->F == 64 && g->layers == 2) return gru::launch<64, 2>(a, s);
     if (g->F == 64) return gru::launch<64, 1>(a, s);

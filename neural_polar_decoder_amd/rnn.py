@@ -28,7 +28,8 @@ class RNN_Model(nn.Module):
     y_h0 in a split precision needs the 16-codeword kernel (hidden 64, 2 layers, N % 32 == 0).  fused_supported(...,
     precision, N) mirrors these limits and npd_rnn_create's LDS bound for hidden 512 x 2 layers.  --use_layernorm nets
     (LayerNorm(F) before the output Linear, rnn_all.py:317-320, :387-398) run on the fp32 GRU kernel at hidden 32 / 64
-    (npd_rnn_create_ex); out_linear_depth > 1 heads are not fused."""
+    (npd_rnn_create_ex); so do --out_linear_depth > 1 heads (Linear(F, H), SELU, ..., Linear(H, 1) with H = y_hidden_size
+    <= 128, rnn_all.py:336-343; each head layer an fp32 MFMA GEMM per decoding step)."""
 
     def __init__(self, rnn_type, input_size, feature_size, output_size, num_rnn_layers, y_size, y_hidden_size,
                  y_depth, activation="relu", dropout=0., skip=False, out_linear_depth=1, y_output_size=None,
@@ -114,8 +115,12 @@ class RNN_Model(nn.Module):
         # LayerNorm head: the fp32 GRU kernel (npd_rnn_create_ex), hidden 32 / 64, unidirectional
         ln_ok = isinstance(self.layernorm, nn.Identity) or (
             isinstance(self.layernorm, nn.LayerNorm) and self.rnn_type == "GRU" and not self.bidirectional
-            and fe in (32, 64) and precision == "fp32")
-        common = self.output_size == 1 and self.out_linear_depth == 1 and ln_ok and self.num_rnn_layers in (1, 2)
+            and fe in (32, 64) and precision == "fp32" and self.out_linear_depth == 1)
+        # out_linear_depth > 1 head: the fp32 GRU kernel, packed hidden 32 / 64, head width y_hidden_size <= 128
+        head_ok = self.out_linear_depth == 1 or (
+            2 <= self.out_linear_depth <= 8 and self.rnn_type == "GRU" and fe in (32, 64) and precision == "fp32"
+            and 1 <= self.y_hidden_size <= 128)
+        common = self.output_size == 1 and head_ok and ln_ok and self.num_rnn_layers in (1, 2)
         if N is not None:
             # npd_gru_create: N a multiple of 8 in [8, 256]; the weight-streaming kernels hold both layers' states and
             # the tile's y in LDS (gru::wide_lds_bytes), so hidden 512 x 2 layers needs N <= 128
@@ -175,16 +180,34 @@ def pack_gru_weights(net: nn.Module, layers: int, y_cols: int = 0) -> np.ndarray
             if nm == "weight_ih" and l == 0 and y_cols:
                 w = np.concatenate([np.zeros((w.shape[0], y_cols), np.float32), w], 1)
             parts.append(w.ravel())
-    parts.append(sd["linear.weight"].ravel())
-    parts.append(sd["linear.bias"].ravel())
+    if net.out_linear_depth == 1:
+        parts.append(sd["linear.weight"].ravel())
+        parts.append(sd["linear.bias"].ravel())
+    else:  # the Linear(F, 1) slot of npd_gru_create's layout is unused: the head goes to npd_rnn_create_ex
+        parts.append(np.zeros((2 if net.bidirectional else 1) * F + 1, np.float32))
     return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
 
 
+def pack_head_weights(net: nn.Module) -> np.ndarray:
+    """The out_linear_depth > 1 head (rnn_all.py:336-343: Sequential(Linear, SELU, ..., Linear)) flattened for
+    npd_rnn_create_ex: each Linear's weight then bias, in order."""
+    lins = [m for m in net.linear if isinstance(m, nn.Linear)]
+    return np.ascontiguousarray(np.concatenate([np.concatenate([m.weight.detach().float().cpu().numpy().ravel(),
+                                                                m.bias.detach().float().cpu().numpy().ravel()])
+                                                for m in lins]), dtype=np.float32)
+
+
 class _GruHandle:
-    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0, cell=0, ln=None):
+    def __init__(self, N, F, layers, onehot, W: np.ndarray, precision=0, cell=0, ln=None, head=None):
         L = _lib.load()
         out = ctypes.c_void_p()
-        if ln is None:
+        if head is not None:  # (depth, hidden, weights) of an out_linear_depth > 1 head
+            d, hid, hw = head
+            _lib.check(L.npd_rnn_create_ex(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
+                                           W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision), None, None,
+                                           0.0, int(d), int(hid), hw.ctypes.data_as(ctypes.c_void_p), int(hw.size),
+                                           ctypes.byref(out)), "npd_rnn_create_ex")
+        elif ln is None:
             _lib.check(L.npd_rnn_create(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
                                         W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision),
                                         ctypes.byref(out)), "npd_rnn_create")
@@ -193,7 +216,7 @@ class _GruHandle:
             _lib.check(L.npd_rnn_create_ex(int(cell), int(N), int(F), int(layers), 1 if onehot else 0,
                                            W.ctypes.data_as(ctypes.c_void_p), int(W.size), int(precision),
                                            g.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p),
-                                           float(eps), ctypes.byref(out)), "npd_rnn_create_ex")
+                                           float(eps), 1, 0, None, 0, ctypes.byref(out)), "npd_rnn_create_ex")
         self.h = out
 
     def __del__(self):
@@ -240,9 +263,12 @@ class RNN_decoder:
             if isinstance(net.layernorm, nn.LayerNorm):
                 ln = (np.ascontiguousarray(net.layernorm.weight.detach().float().cpu().numpy()),
                       np.ascontiguousarray(net.layernorm.bias.detach().float().cpu().numpy()), net.layernorm.eps)
+            head = None
+            if net.out_linear_depth > 1:
+                head = (net.out_linear_depth, net.y_hidden_size, pack_head_weights(net))
             with torch.cuda.device(device):
                 h = _GruHandle(self.N, net.feature_size * (2 if net.bidirectional else 1), net.num_rnn_layers, self.onehot, W,
-                               self.PRECISIONS[self.precision], 1 if net.rnn_type == "LSTM" else 0, ln)
+                               self.PRECISIONS[self.precision], 1 if net.rnn_type == "LSTM" else 0, ln, head)
             self._cache[key] = h
         return h
 

@@ -548,6 +548,39 @@ def gen_gru_ln():
              ln_eps=np.float64(net.layernorm.eps), **{"w." + k: v for k, v in sd.items()})
 
 
+def gen_gru_head():
+    """--out_linear_depth > 1 heads (rnn_all.py:336-343: Linear(F, H), SELU, [Linear(H, H), SELU] ..., Linear(H, 1), H =
+    --y_hidden_size; y_input nets as rnn_all.py:1320 builds them, y_depth 0): depth 2 at hidden 64 x 2 layers with H 64
+    (Polar(32,16), one-hot), depth 3 at hidden 32 x 1 layer with H 48 (Polar(16,8), sign input, reverse order: H padded
+    to 64 by the kernel) and depth 2 at hidden 32 x 2 layers with H 128 (Polar(32,16))."""
+    cases = [("gru_head_polar_32_16_d2_h64", 32, 16, 64, 2, True, False, 2, 64, 320, 4101),
+             ("gru_head_polar_16_8_d3_h48_noonehot_rev", 16, 8, 32, 1, False, True, 3, 48, 256, 4102),
+             ("gru_head_polar_32_16_f32_d2_h128", 32, 16, 32, 2, True, False, 2, 128, 256, 4103)]
+    for name, N, K, F, L, onehot, rev, depth, H, B, seed in cases:
+        torch.manual_seed(seed)
+        code = polar_code(N, K)
+        info = np.asarray(code.info_positions, np.int64)
+        net = rnn_m.RNN_Model("GRU", N + 1 + int(onehot), F, 1, L, N, H, 0, "selu", 0.0, False, out_linear_depth=depth)
+        net.eval()
+        dec = rnn_m.RNN_decoder("y_input", N, info, onehot=onehot, reverse_order=rev)
+        ys, snrs, outs, logits = [], [], [], []
+        rec = []
+        h = net.linear.register_forward_hook(lambda m, i, o: rec.append(o.detach().clone()))
+        for snr in SNRS:
+            msg = 1.0 - 2.0 * torch.randint(0, 2, (B // 5 + 1, K)).float()
+            y = code.channel(code.encode_plotkin(msg), float(snr))
+            rec.clear()
+            with torch.no_grad():
+                d = dec.decode(net, False, y)
+            ys.append(y.numpy()); snrs.append(np.full(y.shape[0], snr)); outs.append(d.numpy())
+            logits.append(torch.stack([r.view(-1) for r in rec], 1).numpy())
+        h.remove()
+        sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+        save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
+             logits=np.concatenate(logits), info=info, N=N, K=K, F=F, layers=L, onehot=int(onehot), rev=int(rev),
+             out_linear_depth=depth, y_hidden=H, **{"w." + k: v for k, v in sd.items()})
+
+
 def gen_gru_ynn():
     """decoding_type 'y_input' with --use_ynn (rnn_all.py:1319-1320: y_output_size = N, the y-MLP's output replaces y as
     the GRU input; decode test branch rnn_all.py:533-536 Fy = net.get_Fy(y), then the y_input loop on [Fy, onehot]):
@@ -731,6 +764,6 @@ def gen_conv():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "gru_ln", "lstm", "lstm_yh0", "rnn_bi", "conv"]
+    which = sys.argv[1:] or ["codes", "encode", "sc", "scl", "scl_long", "lse", "lse_soft", "lse_soft_long", "soft_new", "pac", "errors", "gru", "gru_wide", "gru_yh0", "gru_yh0_skip", "gru_ynn", "gru_ln", "gru_head", "lstm", "lstm_yh0", "rnn_bi", "conv"]
     for w in which:
         globals()["gen_" + w]()

@@ -62,4 +62,6 @@ def test_ln_support_excludes_other_kernels():
     assert not RNN_Model("LSTM", 66, 64, 1, 1, 64, 0, 0, use_layernorm=True).fused_supported("y_input")
     assert not RNN_Model("GRU", 66, 32, 1, 2, 64, 0, 0, bidirectional=True,
                          use_layernorm=True).fused_supported("y_input")
-    assert not RNN_Model("GRU", 66, 64, 1, 2, 64, 64, 0, out_linear_depth=2).fused_supported("y_input")
+    # a LayerNorm in front of an out_linear_depth > 1 head is not fused
+    assert not RNN_Model("GRU", 66, 64, 1, 2, 64, 64, 0, out_linear_depth=2,
+                         use_layernorm=True).fused_supported("y_input")
