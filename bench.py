@@ -171,16 +171,26 @@ def self_launch(args):
 
 
 def dist_setup():
+    """One rank per GPU over RCCL (backend "nccl").  Rehearsal switches for a box with fewer GPUs than ranks (tested by
+    tests/test_bench_launch.py on one MI355X; never used for a reported number): NPD_BENCH_BACKEND=gloo and
+    NPD_BENCH_SHARE_GPU=1 (rank r on GPU r mod device count)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
+        backend = os.environ.get("NPD_BENCH_BACKEND", "nccl")
+        dev_index = local
+        if os.environ.get("NPD_BENCH_SHARE_GPU") == "1":
+            dev_index = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
         if dist.get_world_size() != world:
-            raise SystemExit(f"RCCL world size {dist.get_world_size()} != WORLD_SIZE {world}")
+            raise SystemExit(f"process-group world size {dist.get_world_size()} != WORLD_SIZE {world}")
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -983,6 +993,7 @@ def main():
                    "code": "Polar(64,32) 'polar' rate profile", "batch_per_snr_per_gpu": B, "snr_db": snrs,
                    "parallelism": f"dp{world} (codeword shards; one counter all-reduce)"},
         "world_size_rccl": world, "rank_ms_per_step": rank_ms,
+        "dist_backend": (os.environ.get("NPD_BENCH_BACKEND", "nccl") if world > 1 else None),
         "roofline": {"bound": "mfma",
                      "kernel": "gru16p_kernel<5> (fp16x3 CRISP GRU: the whole SNR sweep in one launch, errors counted "
                                "in the decision epilogue; npd_gru_decode_count_sweep)",
