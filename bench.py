@@ -724,23 +724,28 @@ def conv_leg(dev, rank, world, timer, batch=8192):
                           "dtype": "fp32 (v_mfma_f32_32x32x2_f32)", "achieved_tflops": p32["tf"],
                           "peak_tflops_fp32": FP32_PEAK_TF, "frac": p32["tf"] / FP32_PEAK_TF},
             "config": "configs[4]: Polar(256,128) convNet embed 128, seeded weights",
-            "trained_scaled_down": trained_conv_curve(dev, rank, world)}
+            "trained_scaled_down": trained_conv_curve(dev, rank, world, TRAINED_CONV),
+            "trained_run_alt_e128": trained_conv_curve(dev, rank, world, TRAINED_CONV_E128)}
 
 
 TRAINED_CONV = os.path.join(ROOT, "tests", "golden", "trained_conv_64_22.npz")
+# round 6: run_alt.sh's own width (embed 128, Polar(64,22) n2c; tests/golden/train_conv_gpu.py + gen_trained_conv.py)
+TRAINED_CONV_E128 = os.path.join(ROOT, "tests", "golden", "trained_conv_64_22_e128.npz")
 
 
-def trained_conv_curve(dev, rank, world, n=1 << 18):
-    """The trained conv fixture (embed 16, Polar(64,22), the reference's run_models.py over run_alt.sh's curriculum
-    shape): BER/BLER over 0-4 dB on Philox words, against the reference's own Monte-Carlo curve for the same weights."""
-    if not os.path.exists(TRAINED_CONV):
+def trained_conv_curve(dev, rank, world, path, n=1 << 18, precision="fp16x3"):
+    """A trained conv fixture (embed 16: the reference's run_models.py over run_alt.sh's curriculum shape; embed 128:
+    run_alt.sh's width, stages on the GPU): BER/BLER over 0-4 dB on Philox words through the record's fp16x3 kernels,
+    against the reference's own Monte-Carlo curve for the same weights, with the +-0.05 dB bar (db_bar)."""
+    if not os.path.exists(path):
         return None
     import argparse as _ap
     from neural_polar_decoder_amd import reference_polar_code
     from neural_polar_decoder_amd.models import convNet
-    d = np.load(TRAINED_CONV)
+    d = np.load(path)
     N, K = int(d["N"]), int(d["K"])
-    net = convNet(_ap.Namespace(embed_dim=int(d["embed"]), max_len=N, N=N, dont_use_bias=False, dropout=0.0))
+    net = convNet(_ap.Namespace(embed_dim=int(d["embed"]), max_len=N, N=N, dont_use_bias=False, dropout=0.0),
+                  precision=precision)
     net.load_state_dict({k[2:]: torch.from_numpy(np.asarray(d[k])) for k in d.files if k.startswith("w.")})
     net.eval()
     code = reference_polar_code(N, K)
@@ -761,7 +766,8 @@ def trained_conv_curve(dev, rank, world, n=1 << 18):
     tot = world * n
     ref_bler = [int(x) / int(d["mc_n"]) for x in d["mc_blk_err"]]
     bler = [float(cc[i, 1]) / tot for i in range(len(snrs))]
-    return {"weights": "tests/golden/trained_conv_64_22.npz", "words_per_snr": tot,
+    return {"weights": os.path.relpath(path, ROOT), "precision": precision, "embed": int(d["embed"]),
+            "words_per_snr": tot, "db_bar": db_bar(snrs, bler, tot, ref_bler, int(d["mc_n"])),
             "ber": {str(s_): float(cc[i, 0]) / (tot * K) for i, s_ in enumerate(snrs)},
             "bler": {str(s_): b for s_, b in zip(snrs, bler)},
             "bler_reference": {str(s_): b for s_, b in zip(snrs, ref_bler)},
@@ -1126,6 +1132,9 @@ def compact_configs(legs, gvr):
         cm = legs["conv_model"]
         c["4_conv_model"] = {"value": r3(cm["value"]), "fp16_issued_frac": r3(cm["roofline"]["frac"]),
                              "fp32_path": r3(cm["fp32_path"]["value"])}
+        for k in ("trained_scaled_down", "trained_run_alt_e128"):
+            if cm.get(k):
+                c["4_conv_model"][k + "_ber_match_0.05dB"] = cm[k]["db_bar"]["ber_match_0.05dB"]
     if "montecarlo" in legs:
         c["montecarlo_fused_sc"] = r3(legs["montecarlo"]["value"])
     if "crisp_gru_f512" in legs:

@@ -7,15 +7,17 @@ import os
 import sys
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import trained_fixture
 
-NAME = "trained_conv_64_22"
+NAMES = ["trained_conv_64_22", "trained_conv_64_22_e128"]
 
 
-def test_oracle_conv_trained_fixture(oracle):
-    d = trained_fixture(NAME)
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_conv_trained_fixture(oracle, name):
+    d = trained_fixture(name)
     N, K = int(d["N"]), int(d["K"])
     sd = {k[2:]: np.asarray(d[k]) for k in d.files if k.startswith("w.")}
     info = d["info"]
@@ -41,4 +43,9 @@ def test_oracle_conv_trained_fixture(oracle):
                                                                       "golden", "gen_trained_conv.py"))
     g = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(g)
-    assert [tuple(int(v) for v in r) for r in d["curriculum"]] == [tuple(r) for r in g.CASE["curriculum"]]
+    cur = g.CASES[name]["curriculum"]
+    if cur is None:  # GPU-trained (tests/golden/train_conv_gpu.py holds its curriculum)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+        import train_conv_gpu
+        cur = train_conv_gpu.CASE["curriculum"]
+    assert [tuple(int(v) for v in r) for r in d["curriculum"]] == [tuple(r) for r in cur]

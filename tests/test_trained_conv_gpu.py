@@ -1,9 +1,10 @@
-"""The fused convNet decoder (npd_conv_forward) at trained-model margins (configs[4] scaled down).
+"""The fused convNet decoder (npd_conv_forward) at trained-model margins.
 
-Fixture: tests/golden/trained_conv_64_22.npz -- a convNet (embed 16, Polar(64,22) 'polar' profile) trained with the
-reference's own run_models.py over run_alt.sh's n2c curriculum shape (tests/golden/gen_trained_conv.py), the
-reference's decisions and logits on the fixture words per SNR (0..4 dB) and its Monte-Carlo BER/BLER curve (2^18
-words per SNR through convNet.decode on the CPU).
+Fixtures: tests/golden/trained_conv_64_22.npz -- a convNet (embed 16, Polar(64,22) 'polar' profile) trained with the
+reference's own run_models.py over run_alt.sh's n2c curriculum shape (tests/golden/gen_trained_conv.py) -- and
+trained_conv_64_22_e128.npz, run_alt.sh's own width (embed 128, batch 8192; stages on the GPU by
+tests/golden/train_conv_gpu.py): the reference's decisions and logits on the fixture words per SNR (0..4 dB) and its
+Monte-Carlo BER/BLER curve (2^18 words per SNR through convNet.decode on the CPU).
 
 Tolerance (as tests/test_conv_gpu.py for logits, as tests/test_trained_gru_gpu.py for the curve):
   (a) decisions on the fixture words: >= 99.9 % of information bits and >= 99 % of codewords identical to the
@@ -24,7 +25,10 @@ from conftest import db_offsets, trained_fixture
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 ATOL = 1e-4  # trained weights: the reference's fp32 logits are up to 3.1e-5 from float64 (tests/test_trained_conv.py)
-NAME = "trained_conv_64_22"
+# embed 16 (the reference's run_models.py for every stage) and run_alt.sh's own embed 128 (round 6: every stage on the
+# GPU, tests/golden/train_conv_gpu.py; the configs[4] kernel family -- 64-channel conv_ws16 layers, the 128-channel
+# layer, the 128-tile FC GEMM)
+NAMES = ["trained_conv_64_22", "trained_conv_64_22_e128"]
 
 
 def net_from(d, precision="fp32"):
@@ -52,8 +56,9 @@ def fixture_words(d, si):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
-def test_trained_conv_decisions_match_reference(precision):
-    d = trained_fixture(NAME)
+@pytest.mark.parametrize("name", NAMES)
+def test_trained_conv_decisions_match_reference(name, precision):
+    d = trained_fixture(name)
     net = net_from(d, precision)
     N, K = int(d["N"]), int(d["K"])
     info = d["info"]
@@ -69,9 +74,10 @@ def test_trained_conv_decisions_match_reference(precision):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
-def test_trained_conv_ber_curve_matches_reference(precision):
+@pytest.mark.parametrize("name", NAMES)
+def test_trained_conv_ber_curve_matches_reference(name, precision):
     from neural_polar_decoder_amd import reference_polar_code
-    d = trained_fixture(NAME)
+    d = trained_fixture(name)
     net = net_from(d, precision)
     N, K = int(d["N"]), int(d["K"])
     code = reference_polar_code(N, K)
