@@ -161,3 +161,29 @@ def db_offsets(snrs, bler, ref_snrs, ref_bler, min_bler=1e-4):
         a, b = lr[j], lr[j + 1]
         out.append(float(rs[j] + (lp - a) / (b - a) * (rs[j + 1] - rs[j]) - s))
     return out
+
+
+def assert_db_bar(snrs, bler, n, ref_bler, nr, need=2):
+    """The +-0.05 dB bar on a BLER curve (north_star: within +-0.05 dB of the reference over 0-4 dB): the horizontal
+    offset of our curve from the reference's is defined where the reference's BLER is in [1e-3, 0.9] and resolvable
+    where the two Monte-Carlo samples pin it -- 3 sigma_dB <= 0.05, sigma_dB the binomial sigma of ln BLER of both curves
+    over the reference's local slope |d ln BLER / d SNR|; there |offset| <= 0.05, elsewhere in the domain within its own
+    3 sigma.  At least `need` resolvable points must exist, so the dB bar always runs.  Returns that count."""
+    import numpy as np
+    offs = db_offsets(snrs, bler, snrs, ref_bler, min_bler=1e-3)
+    lr = np.log(np.maximum(ref_bler, 1e-300))
+    checked = 0
+    for i, (s, o, p, pr) in enumerate(zip(snrs, offs, bler, ref_bler)):
+        if not 1e-3 <= pr <= 0.9:
+            continue
+        j0, j1 = max(i - 1, 0), min(i + 1, len(snrs) - 1)
+        slope = abs(lr[j1] - lr[j0]) / (snrs[j1] - snrs[j0])
+        sig = np.sqrt((1 - p) / (p * n) + (1 - pr) / (pr * nr)) / max(slope, 1e-9)
+        assert o is not None, (s, p, pr)
+        if 3 * sig <= 0.05:
+            assert abs(o) <= 0.05, (s, o, pr, sig)
+            checked += 1
+        else:
+            assert abs(o) <= 3 * sig, (s, o, pr, sig)
+    assert checked >= need, f"only {checked} SNR points where the +-0.05 dB bar is defined and resolvable"
+    return checked

@@ -12,7 +12,8 @@ Tolerance (as tests/test_conv_gpu.py for logits, as tests/test_trained_gru_gpu.p
       3.1e-5 from float64, so the seeded nets' 1e-5 bar of tests/test_conv_gpu.py does not apply);
   (b) Monte-Carlo at 2^18 Philox words per SNR: BLER and BER within 4 two-sample standard errors of the reference's
       curve, and the BLER curve's horizontal offset within +-0.05 dB at every point whose reference BLER is in
-      [1e-3, 0.9].
+      [1e-3, 0.9] and where the two samples resolve it (3 sigma_dB <= 0.05; elsewhere in that domain within 3 sigma),
+      at >= 2 such points (conftest.assert_db_bar, as tests/test_trained_gru_gpu.py).
 """
 import argparse
 
@@ -20,7 +21,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import db_offsets, trained_fixture
+from conftest import assert_db_bar, trained_fixture
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -102,10 +103,5 @@ def test_trained_conv_ber_curve_matches_reference(name, precision):
         assert abs(z_bler) < 4 and abs(z_ber) < 4, (s, p, pr, z_bler, z_ber)
         bler.append(p)
     ref_bler = [int(x) / nr for x in d["mc_blk_err"]]
-    offs = db_offsets(snrs, bler, snrs, ref_bler, min_bler=1e-3)
-    checked = 0
-    for s, o, pr in zip(snrs, offs, ref_bler):
-        if 1e-3 <= pr <= 0.9:
-            assert o is not None and abs(o) <= 0.05, (s, o, pr)
-            checked += 1
-    assert checked >= 2, ref_bler
+    # +-0.05 dB where resolvable (at ref BLER ~1e-3 the two 2^18-word samples leave sigma_dB ~0.04: within 3 sigma)
+    assert_db_bar(snrs, bler, n, ref_bler, nr)
