@@ -209,6 +209,18 @@ class GRUMonteCarlo(DecoderMonteCarlo):
     def decisions(self, y):
         return self.decoder.decode(self.net, False, y)
 
+    def count_sweep(self, cw_offset, n, counters):
+        """Every SNR point of the batch in one decode-and-count launch (npd_gru_decode_count_sweep, rnn_all.py:853-880)
+        for y_input nets without the y-MLP; the messages are the same for every point (keyed by codeword)."""
+        if self.decoder.decoding_type != "y_input" or getattr(self.net, "y_depth", 0) > 0:
+            return super().count_sweep(cw_offset, n, counters)
+        y = torch.empty(len(self.snrs), n, self.code.N, dtype=torch.float32, device=self.device)
+        msg = None
+        for si, snr in enumerate(self.snrs):
+            m, _, _ = self.code.mc_generate(n, snr, self.seed, si, cw_offset, want_msg=msg is None, out=y[si])
+            msg = m if msg is None else msg
+        self.decoder.decode_count_sweep(self.net, y, msg, counters, cols=self.info_np)
+
 
 class ConvMonteCarlo(DecoderMonteCarlo):
     """convNet decoding (run_models.py:333-337, testXformer): sign of the LayerNorm output at the info

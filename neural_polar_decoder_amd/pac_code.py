@@ -136,10 +136,12 @@ class PAC:
         return v_hat[:, torch.as_tensor(np.asarray(B), device=v_hat.device)]
 
     # ------------------------------------------------------------------ Monte-Carlo extras
-    def mc_generate(self, Bn, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False):
-        device = torch.device(device or "cuda")
+    def mc_generate(self, Bn, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False, out=None):
+        device = torch.device(device or "cuda") if out is None else out.device
         h = self._code_for(self.B)
-        y = torch.empty(Bn, self.N, dtype=torch.float32, device=device)
+        if out is not None:
+            _lib.check_out(out, "out", torch.float32, Bn * self.N, device)
+        y = torch.empty(Bn, self.N, dtype=torch.float32, device=device) if out is None else out
         msg = torch.empty(Bn, h.K, dtype=torch.float32, device=device) if want_msg else None
         x = torch.empty(Bn, self.N, dtype=torch.float32, device=device) if want_x else None
         _lib.check(_lib.load().npd_mc_generate(h.h, _lib.ptr(msg), _lib.ptr(x), _lib.ptr(y), Bn, sigma_f32(snr),

@@ -279,6 +279,8 @@ class PolarCode:
     # ------------------------------------------------------------------ Monte-Carlo extras
     def mc_generate(self, B, snr, seed, snr_index=0, cw_offset=0, device=None, want_msg=True, want_x=False, out=None):
         device = torch.device(device or "cuda") if out is None else out.device
+        if out is not None:
+            _lib.check_out(out, "out", torch.float32, B * self.N, device)
         y = torch.empty(B, self.N, dtype=torch.float32, device=device) if out is None else out
         msg = torch.empty(B, self.K, dtype=torch.float32, device=device) if want_msg else None
         x = torch.empty(B, self.N, dtype=torch.float32, device=device) if want_x else None

@@ -107,3 +107,43 @@ def test_sweep_rejects_bad_shapes():
         dec.decode_count_sweep(net, y, msg[:, :8], c)      # msg columns != cols
     with pytest.raises(ValueError):
         dec.decode_count_sweep(net, torch.cat([y, y]), msg, c)  # counters too small for 2 segments
+
+
+def test_sweep_non_pm1_messages():
+    """count_errors_kernel compares rint(msg) with rint(decision); the fused count keeps that rule for messages outside
+    {-1, +1} (0 / 1 messages, other integers): the 2-bit codes map -1, +1, 0 and 'other' (never equal to a decision)."""
+    from neural_polar_decoder_amd import reference_polar_code
+    net, dec, d = trained_net("trained_crisp_32_16", "fp16x3")
+    code = reference_polar_code(32, 16)
+    _, y = words(code, [1.0, 2.0], 2000 + 3)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    vals = torch.tensor([-1.0, 1.0, 0.0, 2.0, -3.0, 0.4, -0.6])
+    msg = vals[torch.randint(0, len(vals), (y.shape[1], 16), generator=g)].to(DEV)
+    ref_c, _ = unfused(net, dec, y, msg, np.asarray(code.info_positions))
+    c = torch.zeros(2, 2, dtype=torch.int64, device=DEV)
+    dec.decode_count_sweep(net, y, msg, c)
+    assert torch.equal(c.cpu(), ref_c.cpu())
+
+
+@pytest.mark.parametrize("kind", ["polar", "pac"])
+def test_montecarlo_driver_sweep_equals_per_point(kind):
+    """GRUMonteCarlo.count_sweep (one npd_gru_decode_count_sweep launch per batch, the messages generated once) gives
+    the counters of the per-SNR-point path (generate with message, decode, count) on the same Philox streams."""
+    import argparse
+    from neural_polar_decoder_amd import PAC
+    from neural_polar_decoder_amd.montecarlo import GRUMonteCarlo, MonteCarlo, seeded_crisp
+    if kind == "pac":
+        code = PAC(argparse.Namespace(target_K=64), 128, 64, 91)
+        net, dec = seeded_crisp(code, 64, 2, seed=1, device=DEV, precision="fp16x3")
+    else:
+        net, dec, d = trained_net("trained_crisp_32_16", "fp16x3")
+        from neural_polar_decoder_amd import reference_polar_code
+        code = reference_polar_code(32, 16)
+    mc = GRUMonteCarlo(code, net, dec, [0.0, 2.0, 4.0], 5000, 2048, seed=5, rank=0, world=1, device=DEV)
+    a = mc.new_counters()
+    b = mc.new_counters()
+    for off in range(0, 5000, 2048):
+        n = min(2048, 5000 - off)
+        mc.count_sweep(off, n, a)
+        MonteCarlo.count_sweep(mc, off, n, b)
+    assert torch.equal(a.cpu(), b.cpu()) and int(a[:, 0].sum()) > 0

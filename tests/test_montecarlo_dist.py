@@ -94,7 +94,7 @@ def _oracle_decoder_mc(kind, rank=None, world=None):
     drivers' own."""
     import argparse
     from neural_polar_decoder_amd import PAC, reference_polar_code
-    from neural_polar_decoder_amd.montecarlo import ConvMonteCarlo, GRUMonteCarlo, seeded_conv, seeded_crisp
+    from neural_polar_decoder_amd.montecarlo import ConvMonteCarlo, GRUMonteCarlo, MonteCarlo, seeded_conv, seeded_crisp
     from oracle import oracle as O
     if kind == "gru_pac":
         code = PAC(argparse.Namespace(target_K=64), 128, 64, 91)
@@ -131,6 +131,10 @@ def _oracle_decoder_mc(kind, rank=None, world=None):
             be, bl = O.count_errors(msg.numpy(), np.ascontiguousarray(dec.numpy()[:, self.info_np]))
             row[0] += be
             row[1] += bl
+
+        def count_sweep(self, cw_offset, n, counters):
+            # the per-SNR-point path (GRUMonteCarlo's one-launch sweep is a device kernel: test_gru_sweep_gpu.py)
+            MonteCarlo.count_sweep(self, cw_offset, n, counters)
 
     return _MC(*args, [0.0, 3.0], 300, 64, 77, rank=rank, world=world, device="cpu")
 
