@@ -328,8 +328,10 @@ class RNN_decoder:
         is_info[np.asarray(self.info_inds, np.int64)] = 1
         h = self._handle(net, y.device)
         y = _lib.f32c(y)
-        fused = (self.precision != "fp32" and net.rnn_type == "GRU" and not net.bidirectional and net.feature_size == 64
-                 and net.num_rnn_layers == 2 and self.N % 32 == 0)
+        # the 16-codeword split kernel's handles (npd_gru_create: split precision, packed hidden 64, 2 layers, N % 32 == 0;
+        # a bidirectional hidden-32 net is such a cell) decode and count in one launch without `decoded`
+        fused = (self.precision != "fp32" and net.rnn_type == "GRU" and net.num_rnn_layers == 2 and self.N % 32 == 0
+                 and net.feature_size * (2 if net.bidirectional else 1) == 64)
         if decoded is None and not fused:
             decoded = torch.empty(n, B, self.N, dtype=torch.float32, device=y.device)
         _lib.check_out(decoded, "decoded", torch.float32, n * B * self.N, y.device, optional=True)
