@@ -555,12 +555,15 @@ def gen_gru_head():
     to 64 by the kernel) and depth 2 at hidden 32 x 2 layers with H 128 (Polar(32,16))."""
     cases = [("gru_head_polar_32_16_d2_h64", 32, 16, 64, 2, True, False, 2, 64, 320, 4101),
              ("gru_head_polar_16_8_d3_h48_noonehot_rev", 16, 8, 32, 1, False, True, 3, 48, 256, 4102),
-             ("gru_head_polar_32_16_f32_d2_h128", 32, 16, 32, 2, True, False, 2, 128, 256, 4103)]
+             ("gru_head_polar_32_16_f32_d2_h128", 32, 16, 32, 2, True, False, 2, 128, 256, 4103),
+             ("gru_head_bi_polar_32_16_f32_d2_h64", 32, 16, 32, 2, True, False, 2, 64, 256, 4104)]
     for name, N, K, F, L, onehot, rev, depth, H, B, seed in cases:
         torch.manual_seed(seed)
         code = polar_code(N, K)
         info = np.asarray(code.info_positions, np.int64)
-        net = rnn_m.RNN_Model("GRU", N + 1 + int(onehot), F, 1, L, N, H, 0, "selu", 0.0, False, out_linear_depth=depth)
+        bi = "_bi_" in name  # --bidirectional: the head reads [h_fwd, h_rev] (Linear(2F, H), rnn_all.py:336)
+        net = rnn_m.RNN_Model("GRU", N + 1 + int(onehot), F, 1, L, N, H, 0, "selu", 0.0, False, out_linear_depth=depth,
+                              bidirectional=bi)
         net.eval()
         dec = rnn_m.RNN_decoder("y_input", N, info, onehot=onehot, reverse_order=rev)
         ys, snrs, outs, logits = [], [], [], []
@@ -578,7 +581,7 @@ def gen_gru_head():
         sd = {k: v.detach().numpy() for k, v in net.state_dict().items()}
         save(f"{name}.npz", y=np.concatenate(ys), snr=np.concatenate(snrs), decoded=np.concatenate(outs),
              logits=np.concatenate(logits), info=info, N=N, K=K, F=F, layers=L, onehot=int(onehot), rev=int(rev),
-             out_linear_depth=depth, y_hidden=H, **{"w." + k: v for k, v in sd.items()})
+             out_linear_depth=depth, y_hidden=H, bidirectional=int(bi), **{"w." + k: v for k, v in sd.items()})
 
 
 def gen_gru_ynn():

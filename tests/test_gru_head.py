@@ -9,7 +9,8 @@ import torch
 
 from conftest import golden
 
-CASES = ["gru_head_polar_32_16_d2_h64", "gru_head_polar_16_8_d3_h48_noonehot_rev", "gru_head_polar_32_16_f32_d2_h128"]
+CASES = ["gru_head_polar_32_16_d2_h64", "gru_head_polar_16_8_d3_h48_noonehot_rev", "gru_head_polar_32_16_f32_d2_h128",
+         "gru_head_bi_polar_32_16_f32_d2_h64"]
 
 
 def load(name):
@@ -17,10 +18,29 @@ def load(name):
     return d, {k[2:]: d[k] for k in d.files if k.startswith("w.")}
 
 
+def bi(d):
+    return "bidirectional" in d.files and int(d["bidirectional"]) == 1
+
+
+def model(d):
+    from neural_polar_decoder_amd.rnn import RNN_Model
+    N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
+    return RNN_Model("GRU", N + 1 + int(d["onehot"]), F, 1, L, N, int(d["y_hidden"]), 0, "selu", 0.0, False,
+                     out_linear_depth=int(d["out_linear_depth"]), bidirectional=bi(d))
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_oracle_head_matches_reference(oracle, name):
     d, sd = load(name)
     N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])
+    if bi(d):  # the packed 2F cell (tests/test_rnn_bi.py) under the Sequential head, which reads [h_fwd, h_rev]
+        from test_rnn_bi import packed_state_dict
+        net = model(d)
+        net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        psd = packed_state_dict(net)
+        psd = {k: v for k, v in psd.items() if not k.startswith("linear.")}
+        psd.update({k: v for k, v in sd.items() if k.startswith("linear.")})
+        sd, F = psd, 2 * F
     dec, lg = oracle.gru_decode_f64(d["y"], sd, N, F, L, d["info"], onehot=bool(d["onehot"]), rev=bool(d["rev"]))
     info = d["info"]
     ref = d["decoded"]
@@ -32,15 +52,16 @@ def test_oracle_head_matches_reference(oracle, name):
 
 @pytest.mark.parametrize("name", CASES)
 def test_head_model_loads_and_support_rule(name):
-    from neural_polar_decoder_amd.rnn import RNN_Model, pack_head_weights
+    from neural_polar_decoder_amd.rnn import pack_head_weights
     d, sd = load(name)
-    N, F, L, depth, H = int(d["N"]), int(d["F"]), int(d["layers"]), int(d["out_linear_depth"]), int(d["y_hidden"])
-    net = RNN_Model("GRU", N + 1 + int(d["onehot"]), F, 1, L, N, H, 0, "selu", 0.0, False, out_linear_depth=depth)
+    N, F, depth, H = int(d["N"]), int(d["F"]), int(d["out_linear_depth"]), int(d["y_hidden"])
+    net = model(d)
     net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     assert net.fused_supported("y_input", "fp32", N)
     assert not net.fused_supported("y_input", "fp16x3", N)
     hw = pack_head_weights(net)
-    assert hw.size == H * F + H + (depth - 2) * (H * H + H) + H + 1
+    Fi = F * (2 if bi(d) else 1)
+    assert hw.size == H * Fi + H + (depth - 2) * (H * H + H) + H + 1
 
 
 def test_head_support_limits():

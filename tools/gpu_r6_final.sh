@@ -14,17 +14,17 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
     || { echo "smoke failed"; tail -20 $O/smoke.txt; exit 1; }
   tail -3 $O/smoke.txt
 fi
-timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1 || { echo "bench failed"; tail -30 $O/bench.log; exit 1; }
+timeout -k 10 600 python -u bench.py --full-json $O/bench_full.json ${BENCH_ARGS:-} > $O/bench.log 2>&1 || { echo "bench failed"; tail -30 $O/bench.log; exit 1; }
 tail -n 1 $O/bench.log > $O/bench_line.json
 if [ "${PROF:-1}" = 1 ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
-      python3 bench.py --no-traffic --no-cpu-baseline --steps 5 --warmup 1 > $O/prof.log 2>&1 \
+      python3 bench.py --no-traffic --no-cpu-baseline --steps 5 --warmup 1 --full-json $O/bench_full_prof.json > $O/prof.log 2>&1 \
     || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
   find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/bench_kernel_stats.csv \;
   # the headline step alone (its gru16p_kernel<5> launches are the roofline's; the full run mixes launch sizes)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_headline -o bench -- \
       python3 bench.py --no-traffic --no-cpu-baseline --no-gru --no-pac --no-conv --no-scl --no-lse --no-mc --steps 5 \
-      --warmup 1 > $O/prof_headline.log 2>&1 || { echo "headline prof failed"; tail -20 $O/prof_headline.log; exit 1; }
+      --warmup 1 --full-json $O/bench_full_headline.json > $O/prof_headline.log 2>&1 || { echo "headline prof failed"; tail -20 $O/prof_headline.log; exit 1; }
   find $O/prof_headline -name "*kernel_stats.csv" -exec cp {} $O/bench_headline_kernel_stats.csv \;
 fi
 echo "final done"
