@@ -913,7 +913,11 @@ constexpr int kWspSlots = 3;
 constexpr size_t kFcWspLds = (size_t)kWspSlots * 4 * FB * GSW * 2;
 // PRE: X arrives already split (fp16 hi / lo planes of X 2^SA, row-major like X, written by split_planes_kernel), so the
 // loaders only copy: 16-B loads of both planes into 16-B LDS stores, no split VALU
-template <int FDL, bool PRE>
+// SWZ: the loaders' piece -> (row, chunk) map puts each LDS store's lane group on all 32 write banks.  Stores bank on
+// (a/4) mod 32 in groups of 16 contiguous lanes (ds_write_b64: 2 rows of 8 x 8 B) or 8 (ds_write_b128: 2 rows of
+// 4 x 16 B); at the 20-dword row stride rows r and r + 1 overlap on 4 banks (2-way), rows r and r + 4 start 16 banks
+// apart and tile the 32.  Without it a third of FC0's LDS cycles were conflicts (profiles/round5/pmc_conv_final.json).
+template <int FDL, bool PRE, bool SWZ>
 __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Xhi,
                                                               const uint16_t* __restrict__ Xlo,
                                                               const uint16_t* __restrict__ Whi,
@@ -957,7 +961,10 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
 #pragma unroll
         for (int u = 0; u < UA; ++u) {
             const int idx = lt + NL * u;
-            const int r = idx / A4, c4 = (idx % A4) * (PRE ? 8 : 4);
+            constexpr int GA = PRE ? 8 : 16;  // lanes per store group: 2 rows of A4 pieces
+            const int g = idx / GA, q = idx % GA;
+            const int r = SWZ ? (g >> 2) * 8 + (g & 3) + 4 * (q / A4) : idx / A4;
+            const int c4 = (SWZ ? q % A4 : idx % A4) * (PRE ? 8 : 4);
             const int mr = min(m0 + r, M - 1) - m0;  // row within the block: < 128
             offA[u] = (uint32_t)(((int64_t)mr * K + c4) * (PRE ? 2 : 4));
             ldsA[u] = (uint32_t)(r * GSW + c4);
@@ -965,7 +972,9 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const int idx = lt + NL * u;
-            const int r = idx / B8, c8 = (idx % B8) * 8;
+            const int g = idx / 8, q = idx % 8;
+            const int r = SWZ ? (g >> 2) * 8 + (g & 3) + 4 * (q / B8) : idx / B8;
+            const int c8 = (SWZ ? q % B8 : idx % B8) * 8;
             offB[u] = (uint32_t)(((int64_t)r * K + c8) * 2);
             ldsB[u] = (uint32_t)(r * GSW + c8);
         }
@@ -1119,8 +1128,8 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
     }
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
-#define FC_WSP fc_split_wsp_kernel<NPD_FC_FDL, false>
-#define FC_WSP_PRE fc_split_wsp_kernel<NPD_FC_FDL, true>
+#define FC_WSP(S) fc_split_wsp_kernel<NPD_FC_FDL, false, S>
+#define FC_WSP_PRE(S) fc_split_wsp_kernel<NPD_FC_FDL, true, S>
 
 // X (n floats, n % 4 == 0) -> fp16 planes hi = fp16(x 2^SA), lo = fp16(x 2^SA - hi), SA from the producer's max |x| as
 // in every split consumer (split_sa): the operands fc_split_wsp_kernel<.., true> copies instead of splitting
@@ -1394,6 +1403,11 @@ static bool fc0_presplit() {
     const char* e = getenv("NPD_FC0_PRESPLIT");
     return e != nullptr && atoi(e) != 0;
 }
+// A/B switch NPD_FC_SWZ=0/1 (default 1): the conflict-free loader map of fc_split_wsp_kernel (SWZ above)
+static bool fc_swz() {
+    const char* e = getenv("NPD_FC_SWZ");
+    return e == nullptr || atoi(e) != 0;
+}
 // max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
 // record kLayers + f
 constexpr int kAmaxSlots = kLayers + 3;
@@ -1461,8 +1475,12 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP(false), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP(true), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE(false), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kFcWspLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE(true), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kFcWspLds));
         const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
@@ -1610,12 +1628,14 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                     const int gs = (int)std::min<int64_t>((n4 + 255) / 256, (int64_t)device_cu_count() * 8);
                     hipLaunchKernelGGL(split_planes_kernel, dim3(gs), dim3(256), 0, s, flat, n4, am_in, xh, xl);
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    hipLaunchKernelGGL((FC_WSP_PRE), gb, dim3(512), kFcWspLds, s, fin[f], xh, xl, wh, wl,
+                    auto kern = fc_swz() ? FC_WSP_PRE(true) : FC_WSP_PRE(false);
+                    hipLaunchKernelGGL(kern, gb, dim3(512), kFcWspLds, s, fin[f], xh, xl, wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
                                        am_in, am_out);
                 } else if (fo[f] % FB == 0) {
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    hipLaunchKernelGGL((FC_WSP), gb, dim3(512), kFcWspLds, s, fin[f], nullptr, nullptr, wh, wl,
+                    auto kern = fc_swz() ? FC_WSP(true) : FC_WSP(false);
+                    hipLaunchKernelGGL(kern, gb, dim3(512), kFcWspLds, s, fin[f], nullptr, nullptr, wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
                                        am_in, am_out);
                 } else {

@@ -182,21 +182,24 @@ def test_conv_fp16x3_large_activations(oracle, E, N):
     assert np.array_equal(dec16.cpu().numpy()[::8][sure], np.sign(ref)[sure])
 
 
+@pytest.mark.parametrize("var", ["NPD_FC0_PRESPLIT", "NPD_FC_SWZ"])
 @pytest.mark.parametrize("E,N", [(128, 256), (64, 128)])
-def test_conv_fc0_presplit_identical(monkeypatch, E, N):
-    """NPD_FC0_PRESPLIT (default 1): FC0 reads X as fp16 hi / lo planes split once by split_planes_kernel (the same
+def test_conv_fc0_presplit_identical(monkeypatch, E, N, var):
+    """NPD_FC0_PRESPLIT (default 0): FC0 reads X as fp16 hi / lo planes split once by split_planes_kernel (the same
     x 2^SA split the GEMM's loaders do otherwise) -- logits bit-identical to the in-loader split on a ragged batch of
-    more than one chunk, and at activations beyond fp16's range (the planes carry the same 2^SA scaling)."""
+    more than one chunk, and at activations beyond fp16's range (the planes carry the same 2^SA scaling).
+    NPD_FC_SWZ (default 1): the FC GEMM loaders' conflict-free piece map only moves which lane stores which LDS piece,
+    so the logits are bit-identical with it off."""
     sd = conv_weights_from_seed(E, N, 100 + E)
     net = net_from(sd, E, N, precision="fp16x3")
     rng = np.random.default_rng(3 + E)
     for scale, B in ((1.0, 4096 + 19), (3e4, 129)):
         y = torch.from_numpy((scale * (np.where(rng.random((B, N)) < 0.5, -1.0, 1.0)
                                        + 0.8 * rng.standard_normal((B, N)))).astype(np.float32)).to(DEV)
-        monkeypatch.setenv("NPD_FC0_PRESPLIT", "0")
+        monkeypatch.setenv(var, "0")
         lg0, _ = net.logits(y)
-        monkeypatch.setenv("NPD_FC0_PRESPLIT", "1")
+        monkeypatch.setenv(var, "1")
         lg1, _ = net.logits(y)
-        monkeypatch.delenv("NPD_FC0_PRESPLIT")
+        monkeypatch.delenv(var)
         assert torch.isfinite(lg1).all()
         assert torch.equal(lg0, lg1), float((lg0 - lg1).abs().max())
