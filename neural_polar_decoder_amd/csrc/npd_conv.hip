@@ -32,7 +32,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kLayers = 10;
-constexpr int kChunk = 4096;  // codewords per pass through the layer pipeline
+constexpr int kChunk = 8192;  // codewords per pass through the layer pipeline (FC0: 256-row tiles fill 256 CUs)
 
 struct LayerDesc {
     int cin, cout, dil;
@@ -872,17 +872,16 @@ __global__ __launch_bounds__(256) void fc_split_kernel(const float* __restrict__
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
 
-// fp16x3 FC GEMM with a 128 x 128 block tile (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from N = 128; K is
-// E N, 4 N or N, always a multiple of 32).  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD and its L2):
-// the column tiles of one row block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords at configs[4]
-// -- comes from HBM about once (PMC: 1.8-2.1 GB fetched per FC0 launch against 0.54 GB of X and 8 x 0.13 GB of
-// weight planes, one copy per XCD).  What bounds it (round 5 timing probes, FC0 ~1.0-1.2 ms per 4096 codewords): the
-// operand stream into each CU.  Every K block moves 32 KB (X 16 KB fp32, W 2 x 8 KB fp16) into a CU for 24 MFMAs per
-// wave; with the loads replaced by constants the same kernel ran 0.62 ms, with the MFMAs removed 0.8 ms; deeper
-// register rings (3-6 K blocks), padded row strides and panel-major copies of both operands (16 KB contiguous per K
-// block) all measured within 2 %: ~32 GB/s per CU of mixed L2 / HBM reads, the per-CU load rate MI355X_MICROARCH.md
-// measures for such streams (23-73 GB/s).  Fewer bytes per MFMA need a bigger tile (256 x 128 or 256 x 256), which
-// needs 8192 or 16384 codewords per chunk to fill 256 CUs.
+// fp16x3 FC GEMM with a BM x 128 block tile, BM = 128 or 256 (Nout a multiple of 128: FC0 at every N, FC1 / FC2 from
+// N = 128; K is E N, 4 N or N, always a multiple of 32).  Tiles are dealt XCD by XCD (blocks b, b + 8, ... share an XCD
+// and its L2): the column tiles of one row block run on one XCD, so X -- FC0 streams 537 MB of it per 4096 codewords at
+// configs[4] -- comes from HBM about once (PMC of this kernel: 1.79 GB fetched per 4096-codeword FC0 against the 1.61 GB
+// floor of X once + W once per XCD, profiles/round6/pmc_fc_final.txt).  What bounds it is not settled by any single
+// resource: with the loads replaced by constants it ran 0.62 ms per 4096 codewords, with the MFMAs removed 0.8 ms, both
+// together ~1.0 ms; deeper register rings, padded or panel-major operands (round 5), conflict-free LDS stores, a
+// 256-row tile (25 % fewer operand bytes per MFMA) and fragment reads pinned a k-step ahead (round 6,
+// profiles/round6/fc_tile_ab.txt) all measured within +-5 %.  The loader waves' split VALU shares each SIMD's issue
+// port with the MFMA wave beside it (copy-only loaders on pre-split X: -12 %, fc0_presplit_ab.txt).
 constexpr int FB = 128;
 
 template <int I, int N, class F>
@@ -908,16 +907,21 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
-constexpr int GSW = 40;  // LDS row stride (halfs) of the 32-wide K blocks: 80 B, conflict-free ds_read_b128 rows
 constexpr int kWspSlots = 3;
-constexpr size_t kFcWspLds = (size_t)kWspSlots * 4 * FB * GSW * 2;
+// LDS image of one K block: 64-B rows (32 halfs) with the 16-B chunk q of row r stored at chunk q ^ ((r >> 2) & 3).
+// The MFMA waves' ds_read_b128 (lane -> row col, chunk 2 st + h) then hit all 64 banks in each of its 16-lane groups
+// (rows r and r + 4 of a 256-B bank line differ in the swizzle), and the loaders' stores -- ds_write_b64 of 2 rows x
+// 8 x 8 B per 16 lanes, ds_write_b128 of 2 rows x 4 x 16 B per 8 lanes -- cover the 32 write banks once (bank
+// (a/4) mod 32: two 64-B rows).  Round 5's padded 80-B rows were conflict-free for the reads only (a third of FC0's
+// LDS cycles were store conflicts, profiles/round6/pmc_fc_final.txt) and do not fit three 256-row slots in 160 KB.
+__device__ __forceinline__ int wsp_off(int r, int c) { return r * 32 + ((((c >> 3) ^ (r >> 2)) & 3) << 3) + (c & 7); }
+__host__ __device__ constexpr size_t fc_wsp_lds(int bm) { return (size_t)kWspSlots * (2 * bm + 2 * FB) * 32 * 2; }
 // PRE: X arrives already split (fp16 hi / lo planes of X 2^SA, row-major like X, written by split_planes_kernel), so the
-// loaders only copy: 16-B loads of both planes into 16-B LDS stores, no split VALU
-// SWZ: the loaders' piece -> (row, chunk) map puts each LDS store's lane group on all 32 write banks.  Stores bank on
-// (a/4) mod 32 in groups of 16 contiguous lanes (ds_write_b64: 2 rows of 8 x 8 B) or 8 (ds_write_b128: 2 rows of
-// 4 x 16 B); at the 20-dword row stride rows r and r + 1 overlap on 4 banks (2-way), rows r and r + 4 start 16 banks
-// apart and tile the 32.  Without it a third of FC0's LDS cycles were conflicts (profiles/round5/pmc_conv_final.json).
-template <int FDL, bool PRE, bool SWZ>
+// loaders only copy: 16-B loads of both planes into 16-B LDS stores, no split VALU.
+// BM: rows (codewords) per block tile, 128 or 256, x 128 output features.  BM = 256 moves X 32 KB + W 16 KB per K block
+// for twice the 128-row tile's MFMAs (each MFMA wave owns 128 x 64, TM = 4: 128 accumulator registers, 248 VGPRs); it
+// runs where the chunk gives >= one 256-row tile per CU (npd_conv_forward_ex) at the same speed as BM = 128.
+template <int FDL, bool PRE, int BM>
 __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __restrict__ X, const uint16_t* __restrict__ Xhi,
                                                               const uint16_t* __restrict__ Xlo,
                                                               const uint16_t* __restrict__ Whi,
@@ -928,13 +932,15 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
                                                               uint32_t* __restrict__ amax_out) {
     constexpr int GKT = 32, NS = kWspSlots;
     static_assert(FDL >= 2 && FDL % NS == 0, "the prologue stashes two K blocks; LDS slots repeat with the ring");
+    static_assert(BM == 128 || BM == 256, "block tile rows");
     constexpr int NL = 256;                            // loader threads
     constexpr int A4 = PRE ? GKT / 8 : GKT / 4, B8 = GKT / 8;  // 16-B pieces per A row (per plane), per B row
-    constexpr int UA = FB * A4 / NL, UB = FB * B8 / NL;  // 4 (fp32 X) or 2 per plane (PRE), 2
-    constexpr int TM = 2, TN = 2;
-    constexpr int PL = FB * GSW;  // halfs per plane
+    constexpr int UA = BM * A4 / NL, UB = FB * B8 / NL;
+    constexpr int TM = BM / 64, TN = 2;
+    constexpr int PA = BM * 32, PB = FB * 32;  // halfs per A plane, per B plane
+    constexpr int SLOT = 2 * PA + 2 * PB;
     const uint32_t am_raw = amax_in != nullptr ? __builtin_nontemporal_load(amax_in + (threadIdx.x & 63) * kAmaxStride) : 0u;
-    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [slot][A hi, A lo, B hi, B lo][128][GSW]
+    extern __shared__ __attribute__((aligned(16))) _Float16 smb[];  // [slot][A hi, A lo (BM rows), B hi, B lo (128)][32]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const bool loader = wave >= 4;
@@ -942,7 +948,7 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
     const int total = gridDim.x;
     int lin = blockIdx.x;
     if ((total & 7) == 0) lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-    const int m0 = (lin / gx) * FB, j0 = (lin % gx) * FB;
+    const int m0 = (lin / gx) * BM, j0 = (lin % gx) * FB;
     const int nk = K / GKT;
     const int sa = amax_in != nullptr ? min(kSplitSA, 15 - ((int)((wave_max_u32(am_raw) >> 23) & 0xFFu) - 126)) : kSplitSA;
     const float sa_scale = __builtin_ldexpf(1.0f, sa), descale = __builtin_ldexpf(1.0f, -(sw + sa));
@@ -951,7 +957,8 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
         const int lt = tid - 256;
         // per-lane byte offsets (fixed for the launch) against wave-uniform K-block bases: one 32-bit address register
         // per load, no 64-bit address arithmetic per K block.  The offsets are relative to the block's first row of X
-        // and of W (64-bit bases), so they stay below 128 K 4 B < 2^28 at the largest accepted K = 512 x 1024
+        // and of W (64-bit bases), so they stay below 256 K 4 B < 2^29 at the largest accepted K = 512 x 1024.
+        // Piece idx -> row idx / A4: 16 (8) consecutive lanes store 2 whole rows, conflict-free (wsp_off)
         const char* const xblk = reinterpret_cast<const char*>(X) + (size_t)m0 * K * 4;
         const char* const xhblk = reinterpret_cast<const char*>(Xhi) + (size_t)m0 * K * 2;
         const char* const xlblk = reinterpret_cast<const char*>(Xlo) + (size_t)m0 * K * 2;
@@ -961,22 +968,17 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
 #pragma unroll
         for (int u = 0; u < UA; ++u) {
             const int idx = lt + NL * u;
-            constexpr int GA = PRE ? 8 : 16;  // lanes per store group: 2 rows of A4 pieces
-            const int g = idx / GA, q = idx % GA;
-            const int r = SWZ ? (g >> 2) * 8 + (g & 3) + 4 * (q / A4) : idx / A4;
-            const int c4 = (SWZ ? q % A4 : idx % A4) * (PRE ? 8 : 4);
-            const int mr = min(m0 + r, M - 1) - m0;  // row within the block: < 128
+            const int r = idx / A4, c4 = (idx % A4) * (PRE ? 8 : 4);
+            const int mr = min(m0 + r, M - 1) - m0;  // row within the block: < BM
             offA[u] = (uint32_t)(((int64_t)mr * K + c4) * (PRE ? 2 : 4));
-            ldsA[u] = (uint32_t)(r * GSW + c4);
+            ldsA[u] = (uint32_t)wsp_off(r, c4);
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const int idx = lt + NL * u;
-            const int g = idx / 8, q = idx % 8;
-            const int r = SWZ ? (g >> 2) * 8 + (g & 3) + 4 * (q / B8) : idx / B8;
-            const int c8 = (SWZ ? q % B8 : idx % B8) * 8;
+            const int r = idx / B8, c8 = (idx % B8) * 8;
             offB[u] = (uint32_t)(((int64_t)r * K + c8) * 2);
-            ldsB[u] = (uint32_t)(r * GSW + c8);
+            ldsB[u] = (uint32_t)wsp_off(r, c8);
         }
         f4 ra[FDL][UA], ral[FDL][PRE ? UA : 1], rbh[FDL][UB], rbl[FDL][UB];
         auto fetch = [&](int slot, int kb) {
@@ -1001,12 +1003,12 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
             }
         };
         auto stash = [&](int slot, auto lds_slot) {
-            _Float16* const base = smb + (size_t)decltype(lds_slot)::value * 4 * PL;
+            _Float16* const base = smb + (size_t)decltype(lds_slot)::value * SLOT;
             if constexpr (PRE) {
 #pragma unroll
                 for (int u = 0; u < UA; ++u) {
                     *reinterpret_cast<f4*>(base + ldsA[u]) = ra[slot][u];
-                    *reinterpret_cast<f4*>(base + PL + ldsA[u]) = ral[slot][u];
+                    *reinterpret_cast<f4*>(base + PA + ldsA[u]) = ral[slot][u];
                 }
             } else
 #pragma unroll
@@ -1019,12 +1021,12 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
                     lo[e] = (_Float16)(x - (float)hi[e]);
                 }
                 *reinterpret_cast<hf4*>(base + ldsA[u]) = hi;
-                *reinterpret_cast<hf4*>(base + PL + ldsA[u]) = lo;
+                *reinterpret_cast<hf4*>(base + PA + ldsA[u]) = lo;
             }
 #pragma unroll
             for (int u = 0; u < UB; ++u) {
-                *reinterpret_cast<f4*>(base + 2 * PL + ldsB[u]) = rbh[slot][u];
-                *reinterpret_cast<f4*>(base + 3 * PL + ldsB[u]) = rbl[slot][u];
+                *reinterpret_cast<f4*>(base + 2 * PA + ldsB[u]) = rbh[slot][u];
+                *reinterpret_cast<f4*>(base + 2 * PA + PB + ldsB[u]) = rbl[slot][u];
             }
         };
         // block b lives in register slot b % FDL from its fetch to its stash into LDS slot b % NS
@@ -1060,21 +1062,25 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
 #pragma unroll
             for (int b = 0; b < TN; ++b)
                 acc[a][b] = f16v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        const int ar = (wm * 32 * TM + col) * GSW + 8 * h, br = (wn * 32 * TN + col) * GSW + 8 * h;
+        // fragment rows wm 32 TM + 32 t + col (A) and wn 64 + 32 t + col (B): every tile base is a multiple of 32, so
+        // the swizzle of chunk 2 st + h depends on col only
+        const int xr = (col >> 2) & 3;
+        const int cq0 = ((0 + h) ^ xr) << 3, cq1 = ((2 + h) ^ xr) << 3;
+        const int ar = (wm * 32 * TM + col) * 32, br = (wn * 32 * TN + col) * 32;
         struct Frags {
             hf8 ah[TM], al[TM], bh[TN], bl[TN];
         };
         auto read = [&](int slot, int st, Frags& f) {
-            const _Float16* const cb = smb + (size_t)slot * 4 * PL + 16 * st;
+            const _Float16* const cb = smb + (size_t)slot * SLOT + (st ? cq1 : cq0);
 #pragma unroll
             for (int t = 0; t < TM; ++t) {
-                f.ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * GSW);
-                f.al[t] = *reinterpret_cast<const hf8*>(cb + PL + ar + t * 32 * GSW);
+                f.ah[t] = *reinterpret_cast<const hf8*>(cb + ar + t * 32 * 32);
+                f.al[t] = *reinterpret_cast<const hf8*>(cb + PA + ar + t * 32 * 32);
             }
 #pragma unroll
             for (int t = 0; t < TN; ++t) {
-                f.bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PL + br + t * 32 * GSW);
-                f.bl[t] = *reinterpret_cast<const hf8*>(cb + 3 * PL + br + t * 32 * GSW);
+                f.bh[t] = *reinterpret_cast<const hf8*>(cb + 2 * PA + br + t * 32 * 32);
+                f.bl[t] = *reinterpret_cast<const hf8*>(cb + 2 * PA + PB + br + t * 32 * 32);
             }
         };
         Frags f[2];
@@ -1128,8 +1134,8 @@ __global__ __launch_bounds__(512, 1) void fc_split_wsp_kernel(const float* __res
     }
     if (amax_out != nullptr) publish_amax(amax_out, amx);
 }
-#define FC_WSP(S) fc_split_wsp_kernel<NPD_FC_FDL, false, S>
-#define FC_WSP_PRE(S) fc_split_wsp_kernel<NPD_FC_FDL, true, S>
+#define FC_WSP(BMV) fc_split_wsp_kernel<NPD_FC_FDL, false, BMV>
+#define FC_WSP_PRE fc_split_wsp_kernel<NPD_FC_FDL, true, 128>
 
 // X (n floats, n % 4 == 0) -> fp16 planes hi = fp16(x 2^SA), lo = fp16(x 2^SA - hi), SA from the producer's max |x| as
 // in every split consumer (split_sa): the operands fc_split_wsp_kernel<.., true> copies instead of splitting
@@ -1403,12 +1409,11 @@ static bool fc0_presplit() {
     const char* e = getenv("NPD_FC0_PRESPLIT");
     return e != nullptr && atoi(e) != 0;
 }
-// A/B switch NPD_FC_SWZ=0/1 (default 1): the conflict-free loader map of fc_split_wsp_kernel (SWZ above)
-static bool fc_swz() {
-    const char* e = getenv("NPD_FC_SWZ");
-    return e == nullptr || atoi(e) != 0;
-}
-// max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
+// A/B switch NPD_FC_BM = 128 / 256 (default 0: automatic): FC block-tile rows, see fc_split_wsp_kernel
+static int fc_bm_env() {
+    const char* e = getenv("NPD_FC_BM");
+    return e == nullptr ? 0 : atoi(e);
+}// max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
 // record kLayers + f
 constexpr int kAmaxSlots = kLayers + 3;
 
@@ -1475,12 +1480,12 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                                     163840));
         NPD_HIP(hipFuncSetAttribute((const void*)conv_layer_split_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     163840));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP(false), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP(true), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFcWspLds));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE(false), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kFcWspLds));
-        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE(true), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kFcWspLds));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP(128), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)fc_wsp_lds(128)));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP(256), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)fc_wsp_lds(256)));
+        NPD_HIP(hipFuncSetAttribute((const void*)FC_WSP_PRE, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)fc_wsp_lds(128)));
         const void* ws[8] = {(const void*)conv_split_ws_kernel<1, 1, 1, 4>, (const void*)conv_split_ws_kernel<1, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<2, 1, 1, 4>, (const void*)conv_split_ws_kernel<2, 2, 1, 4>,
                              (const void*)conv_split_ws_kernel<3, 1, 1, 4>, (const void*)conv_split_ws_kernel<3, 2, 1, 4>,
@@ -1628,14 +1633,17 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                     const int gs = (int)std::min<int64_t>((n4 + 255) / 256, (int64_t)device_cu_count() * 8);
                     hipLaunchKernelGGL(split_planes_kernel, dim3(gs), dim3(256), 0, s, flat, n4, am_in, xh, xl);
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    auto kern = fc_swz() ? FC_WSP_PRE(true) : FC_WSP_PRE(false);
-                    hipLaunchKernelGGL(kern, gb, dim3(512), kFcWspLds, s, fin[f], xh, xl, wh, wl,
+                    hipLaunchKernelGGL(FC_WSP_PRE, gb, dim3(512), fc_wsp_lds(128), s, fin[f], xh, xl, wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
                                        am_in, am_out);
                 } else if (fo[f] % FB == 0) {
-                    dim3 gb((unsigned)((fo[f] / FB) * ((nb + FB - 1) / FB)));
-                    auto kern = fc_swz() ? FC_WSP(true) : FC_WSP(false);
-                    hipLaunchKernelGGL(kern, gb, dim3(512), kFcWspLds, s, fin[f], nullptr, nullptr, wh, wl,
+                    // 256-row tiles where they alone give every CU a tile (FC0 of an 8192-codeword chunk at N >= 256),
+                    // else 128 x 128
+                    const int64_t t256 = (fo[f] / FB) * ((nb + 255) / 256);
+                    const int bm = fc_bm_env() ? fc_bm_env() : (t256 >= device_cu_count() ? 256 : 128);
+                    dim3 gb((unsigned)((fo[f] / FB) * ((nb + bm - 1) / bm)));
+                    auto kern = bm == 256 ? FC_WSP(256) : FC_WSP(128);
+                    hipLaunchKernelGGL(kern, gb, dim3(512), fc_wsp_lds(bm), s, fin[f], nullptr, nullptr, wh, wl,
                                        c->img + c->off_fc[f][1], fout[f], (int)nb, fk[f], fo[f], fa[f], c->fc_sw[f],
                                        am_in, am_out);
                 } else {

@@ -61,7 +61,7 @@ def test_conv_vs_oracle_ragged_batch(oracle):
     sd = {k[2:]: d[k] for k in d.files if k.startswith("w.")}
     net = net_from(sd, int(d["embed"]), int(d["N"]))
     rng = np.random.default_rng(1)
-    y = rng.standard_normal((4096 + 77, 64)).astype(np.float32)  # > one chunk, ragged tail
+    y = rng.standard_normal((8192 + 77, 64)).astype(np.float32)  # > one chunk, ragged tail
     lg, dec = net.logits(torch.from_numpy(y).to(DEV))
     ref = oracle.conv_forward(y[::37], sd)
     check(lg.cpu().numpy()[::37], dec.cpu().numpy()[::37], ref)
@@ -82,9 +82,9 @@ def test_conv_forward_returns_input4(oracle):
     assert np.abs(in4.cpu().numpy() - o4).max() < ATOL
     check(logits.squeeze(-1).cpu().numpy(), dec.squeeze(-1).cpu().numpy(), d["logits"])
     assert out.shape == (y.shape[0], int(d["N"]), 2)
-    # ragged batch over more than one 4096-codeword chunk
+    # ragged batch over more than one 8192-codeword chunk
     rng = np.random.default_rng(2)
-    yb = rng.standard_normal((4096 + 33, 64)).astype(np.float32)
+    yb = rng.standard_normal((8192 + 33, 64)).astype(np.float32)
     _, _, b4 = net.logits(torch.from_numpy(yb).to(DEV), want_input4=True)
     _, o4b = oracle.conv_forward(yb[::41], sd, want_input4=True)
     assert np.abs(b4.cpu().numpy()[::41] - o4b).max() < ATOL
@@ -141,7 +141,7 @@ def test_conv_fp16x3_error_matches_fp32_against_float64(oracle):
 @pytest.mark.parametrize("E,N", [(64, 128), (64, 64), (80, 64), (96, 64), (128, 256)])
 def test_conv_fp16x3_shapes_vs_oracle(oracle, E, N):
     """The fp16x3 kernels at every shape family they dispatch on, against the float64 oracle on a ragged batch of more
-    than one 4096-codeword chunk (seeded weights, conftest.conv_weights_from_seed): embed 64 / N 128 (weight-stationary
+    than one 8192-codeword chunk (seeded weights, conftest.conv_weights_from_seed): embed 64 / N 128 (weight-stationary
     conv kernel with 32-channel groups, 128-position items; the 128 x 128 FC kernel for all three Linear layers); embed
     64 / N 64 (the 64-channel layer on 64-position items);
     embed 80 / N 64 (40-channel layers = three 16-channel groups, 64-position items; the 80-channel layer on the
@@ -152,7 +152,7 @@ def test_conv_fp16x3_shapes_vs_oracle(oracle, E, N):
     sd = conv_weights_from_seed(E, N, 100 + E)
     net = net_from(sd, E, N, precision="fp16x3")
     rng = np.random.default_rng(E + N)
-    B = 4096 + 37
+    B = 8192 + 37
     y = (np.where(rng.random((B, N)) < 0.5, -1.0, 1.0) + 0.8 * rng.standard_normal((B, N))).astype(np.float32)
     lg, dec = net.logits(torch.from_numpy(y).to(DEV))
     sel = np.r_[0:B:97, B - 1]
@@ -182,23 +182,23 @@ def test_conv_fp16x3_large_activations(oracle, E, N):
     assert np.array_equal(dec16.cpu().numpy()[::8][sure], np.sign(ref)[sure])
 
 
-@pytest.mark.parametrize("var", ["NPD_FC0_PRESPLIT", "NPD_FC_SWZ"])
+@pytest.mark.parametrize("var,v0,v1", [("NPD_FC0_PRESPLIT", "0", "1"), ("NPD_FC_BM", "128", "256")])
 @pytest.mark.parametrize("E,N", [(128, 256), (64, 128)])
-def test_conv_fc0_presplit_identical(monkeypatch, E, N, var):
+def test_conv_fc0_presplit_identical(monkeypatch, E, N, var, v0, v1):
     """NPD_FC0_PRESPLIT (default 0): FC0 reads X as fp16 hi / lo planes split once by split_planes_kernel (the same
     x 2^SA split the GEMM's loaders do otherwise) -- logits bit-identical to the in-loader split on a ragged batch of
     more than one chunk, and at activations beyond fp16's range (the planes carry the same 2^SA scaling).
-    NPD_FC_SWZ (default 1): the FC GEMM loaders' conflict-free piece map only moves which lane stores which LDS piece,
-    so the logits are bit-identical with it off."""
+    NPD_FC_BM (default: 256-row tiles where they fill every CU): the FC GEMM's 128- and 256-row block tiles sum every
+    output over the same K order on the same 32 x 32 MFMA tiles, so the logits are bit-identical."""
     sd = conv_weights_from_seed(E, N, 100 + E)
     net = net_from(sd, E, N, precision="fp16x3")
     rng = np.random.default_rng(3 + E)
-    for scale, B in ((1.0, 4096 + 19), (3e4, 129)):
+    for scale, B in ((1.0, 8192 + 19), (3e4, 129)):
         y = torch.from_numpy((scale * (np.where(rng.random((B, N)) < 0.5, -1.0, 1.0)
                                        + 0.8 * rng.standard_normal((B, N)))).astype(np.float32)).to(DEV)
-        monkeypatch.setenv(var, "0")
+        monkeypatch.setenv(var, v0)
         lg0, _ = net.logits(y)
-        monkeypatch.setenv(var, "1")
+        monkeypatch.setenv(var, v1)
         lg1, _ = net.logits(y)
         monkeypatch.delenv(var)
         assert torch.isfinite(lg1).all()
