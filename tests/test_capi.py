@@ -109,3 +109,41 @@ def test_list_prune_select_host_utility_matches_std_nth_element(oracle):
     assert L.npd_list_prune_select(None, 4, 2, ctypes.byref(m)) < 0
     v = np.zeros(20, np.float32)
     assert L.npd_list_prune_select(v.ctypes.data_as(ctypes.c_void_p), 20, 2, ctypes.byref(m)) < 0
+
+
+def test_every_entry_point_rejects_null_operands():
+    """Every compute and create entry point, called with NULL for each pointer (handles, operands, out-handles) and
+    small valid sizes, returns a negative status with a message -- checked before any HIP call, so it runs without a
+    GPU; destroy(NULL) is a no-op.  Run in a child process, so a crash fails this test instead of the session."""
+    script = r'''
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+from neural_polar_decoder_amd import _lib
+L = _lib.load()
+skip = {"npd_abi_version", "npd_last_error", "npd_device_count", "npd_conv_workspace_bytes",
+        "npd_code_destroy", "npd_gru_destroy", "npd_conv_destroy"}
+bad = []
+for name, res, argt in _lib.SIGNATURES:
+    if name in skip:
+        continue
+    args = []
+    for t in argt:
+        if t in (ctypes.c_int, ctypes.c_uint):
+            args.append(16)
+        elif t in (ctypes.c_long, ctypes.c_ulong):
+            args.append(16)
+        elif t is ctypes.c_float:
+            args.append(1.0)
+        else:
+            args.append(None)
+    rc = getattr(L, name)(*args)
+    if not (rc < 0 and L.npd_last_error()):
+        bad.append((name, rc))
+for d in ("npd_code_destroy", "npd_gru_destroy", "npd_conv_destroy"):
+    if getattr(L, d)(None) != 0:
+        bad.append((d, "destroy(NULL)"))
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+'''
+    r = subprocess.run([os.sys.executable, "-c", script, ROOT], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
