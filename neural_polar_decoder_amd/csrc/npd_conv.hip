@@ -1399,7 +1399,13 @@ extern "C" int npd_conv_destroy(npd_conv* c) {
     return NPD_OK;
 }
 
-static int64_t chunk_of(int64_t B) { return B < kChunk ? B : kChunk; }
+// codewords per pass: kChunk, halved (to >= 512) while the three (chunk, E, N) fp32 activation buffers would pass
+// 4 GiB -- configs[4] (E N = 32768) keeps 8192 (3.2 GB); the widest accepted net (E 512, N 1024) runs 512
+static int64_t chunk_of(const npd_conv* c, int64_t B) {
+    int64_t ch = kChunk;
+    while (ch > 512 && 3 * ch * (int64_t)c->E * c->N * 4 > ((int64_t)4 << 30)) ch >>= 1;
+    return B < ch ? B : ch;
+}
 // A/B switch NPD_FC0_PRESPLIT=0/1 (default 0): FC0 on pre-split X planes (split_planes_kernel + fc_split_wsp_kernel<..,
 // true>).  Round 6 (profiles/round6/fc0_presplit_ab.txt): with copy-only loaders FC0 takes 935-938 us
 // per 4096 codewords against 1,061 us splitting in its loaders (-12 %), but the separate split pass costs 197 us, so the
@@ -1440,7 +1446,7 @@ __global__ __launch_bounds__(256) void act_to_channels_first_kernel(const float*
 
 extern "C" int64_t npd_conv_workspace_bytes(const npd_conv* c, int64_t B) {
     if (!c || B <= 0) return 0;
-    const int64_t Bc = chunk_of(B);
+    const int64_t Bc = chunk_of(c, B);
     // three activation buffers of (Bc, E, N) + FC1/FC2/FC3 outputs + the activation-range words (kAmaxSlots)
     return (3 * Bc * (int64_t)c->E * c->N + Bc * 4 * (int64_t)c->N + 2 * Bc * (int64_t)c->N) * 4 + 256 + (int64_t)kAmaxSlots * kAmaxWords * 4;
 }
@@ -1462,7 +1468,7 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
     NPD_ARG(logits != nullptr || decoded != nullptr, "npd_conv_forward: nothing to write");
     hipStream_t s = (hipStream_t)stream;
     const int N = c->N, E = c->E;
-    const int64_t Bc = chunk_of(B);
+    const int64_t Bc = chunk_of(c, B);
     float* ws = reinterpret_cast<float*>(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
     float* A0 = ws;
     float* A1 = A0 + Bc * (int64_t)E * N;

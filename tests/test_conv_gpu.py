@@ -203,3 +203,20 @@ def test_conv_fc0_presplit_identical(monkeypatch, E, N, var, v0, v1):
         monkeypatch.delenv(var)
         assert torch.isfinite(lg1).all()
         assert torch.equal(lg0, lg1), float((lg0 - lg1).abs().max())
+
+
+def test_conv_wide_shape_smaller_chunk_vs_oracle(oracle):
+    """embed 128 / N 512 (FC0 K = 65536 into 2048 features): npd_conv_forward halves its 8192-codeword chunk while the
+    three activation buffers would pass 4 GiB, so this batch runs in 4096-codeword chunks (the second one ragged);
+    FC0's per-lane LDS / global offsets stay block-relative at this K.  fp16x3 and fp32 against the float64
+    oracle on rows of both chunks, the same bars as the other shapes."""
+    E, N = 128, 512
+    sd = conv_weights_from_seed(E, N, 7)
+    rng = np.random.default_rng(17)
+    B = 4096 + 21
+    y = (np.where(rng.random((B, N)) < 0.5, -1.0, 1.0) + 0.8 * rng.standard_normal((B, N))).astype(np.float32)
+    sel = np.array([0, 2047, 4095, 4096, B - 1])
+    ref = oracle.conv_forward(y[sel], sd)
+    for prec in ("fp16x3", "fp32"):
+        lg, dec = net_from(sd, E, N, precision=prec).logits(torch.from_numpy(y).to(DEV))
+        check(lg.cpu().numpy()[sel], dec.cpu().numpy()[sel], ref)
