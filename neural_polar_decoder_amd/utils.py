@@ -37,8 +37,9 @@ def count_errors(y_true: torch.Tensor, y_pred: torch.Tensor, counters: torch.Ten
     dev = counters.device if counters is not None and counters.is_cuda else None
     t = _lib.stage(y_true, "y_true", dev)
     p = _lib.stage(y_pred, "y_pred", t.device)
-    t = _lib.f32c(t.reshape(t.shape[0], -1))
-    p = _lib.f32c(p.reshape(p.shape[0], -1))
+    # explicit widths: an empty batch (B = 0) is a no-op, not an ambiguous reshape
+    t = _lib.f32c(t.reshape(t.shape[0], int(np.prod(t.shape[1:], dtype=np.int64))))
+    p = _lib.f32c(p.reshape(p.shape[0], int(np.prod(p.shape[1:], dtype=np.int64))))
     if counters is None:
         counters = torch.zeros(2, dtype=torch.int64, device=t.device)
     _lib.require_gpu(counters, "counters")
@@ -47,12 +48,16 @@ def count_errors(y_true: torch.Tensor, y_pred: torch.Tensor, counters: torch.Ten
         c = np.ascontiguousarray(np.asarray(cols, dtype=np.int64).reshape(-1), dtype=np.int32)
         if t.shape[0] != p.shape[0] or c.size != t.shape[1]:
             raise ValueError(f"shape mismatch {tuple(t.shape)} vs {tuple(p.shape)} at {c.size} columns")
+        if t.shape[0] == 0:
+            return counters
         _lib.check(L.npd_count_errors_cols(_lib.ptr(t), _lib.ptr(p), t.shape[0], t.shape[1], p.shape[1],
                                            c.ctypes.data_as(_lib.c_void_p), _lib.ptr(counters),
                                            _lib.stream_of(t.device)), "npd_count_errors_cols")
         return counters
     if t.shape != p.shape:
         raise ValueError(f"shape mismatch {tuple(t.shape)} vs {tuple(p.shape)}")
+    if t.shape[0] == 0:
+        return counters
     _lib.check(L.npd_count_errors(_lib.ptr(t), _lib.ptr(p), t.shape[0], t.shape[1], _lib.ptr(counters),
                                   _lib.stream_of(t.device)), "npd_count_errors")
     return counters
@@ -79,6 +84,7 @@ def errors_ber(y_true, y_pred, mask=None):
     rounded quotient of the true counts.  An integer mask (the loops' torch.ones(...).long()) is counted by
     npd_count_errors_masked -- sum(mask * err) / sum(mask), decided on the device with no host read of the mask
     (an all-ones mask costs the same single pass); a floating-point mask takes the reference's formula on the GPU."""
+    y_true.view(y_true.shape[0], -1, 1)  # the reference's first step (utils.py:20): raises on an empty batch as there
     if mask is not None:
         t = _lib.f32c(_lib.stage(y_true, "y_true"))
         if mask.dtype.is_floating_point or mask.dtype.is_complex:
@@ -114,6 +120,7 @@ def errors_bler(y_true, y_pred, get_pos=False):
     Returns ``numpy.float64`` like the reference (its loops call ``.item()`` on it, rnn_all.py:856,
     run_models.py:331); with ``get_pos`` also the list of erroneous row indices (numpy int64)."""
     B = y_true.shape[0]
+    y_true.view(B, -1, 1)  # the reference's first step (utils.py:38): raises on an empty batch as there
     if get_pos:
         e, _ = _masked_errors(y_true, y_pred, torch.ones(1, dtype=torch.float32).expand(B, 1))
         bad = (e.reshape(B, -1).sum(1) > 0).cpu().numpy()
