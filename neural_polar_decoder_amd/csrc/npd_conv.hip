@@ -1418,7 +1418,8 @@ static bool fc0_presplit() {
 // A/B switch NPD_FC_BM = 128 / 256 (default 0: automatic): FC block-tile rows, see fc_split_wsp_kernel
 static int fc_bm_env() {
     const char* e = getenv("NPD_FC_BM");
-    return e == nullptr ? 0 : atoi(e);
+    const int v = e == nullptr ? 0 : atoi(e);
+    return v == 128 || v == 256 ? v : 0;  // anything else: automatic (the grid is sized for the tile actually launched)
 }// max |activation| records of one chunk (fp16x3; kAmaxWords words each): conv layer i's output at record i, FC f's at
 // record kLayers + f
 constexpr int kAmaxSlots = kLayers + 3;
@@ -1646,7 +1647,8 @@ extern "C" int npd_conv_forward_ex(const npd_conv* c, const float* y, float* log
                     // 256-row tiles where they alone give every CU a tile (FC0 of an 8192-codeword chunk at N >= 256),
                     // else 128 x 128
                     const int64_t t256 = (fo[f] / FB) * ((nb + 255) / 256);
-                    const int bm = fc_bm_env() ? fc_bm_env() : (t256 >= device_cu_count() ? 256 : 128);
+                    const int bm_env = fc_bm_env();
+                    const int bm = bm_env ? bm_env : (t256 >= device_cu_count() ? 256 : 128);
                     dim3 gb((unsigned)((fo[f] / FB) * ((nb + bm - 1) / bm)));
                     auto kern = bm == 256 ? FC_WSP(256) : FC_WSP(128);
                     hipLaunchKernelGGL(kern, gb, dim3(512), fc_wsp_lds(bm), s, fin[f], nullptr, nullptr, wh, wl,
