@@ -68,7 +68,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])  # 3: shards of unequal size (3000 words)
 def test_gloo_sharded_equals_single_process(world):
     from oracle import oracle as O
     O.set_num_threads(2)
