@@ -121,8 +121,10 @@ def trained_words(d, si):
     torch.manual_seed(int(d["seed_dec"]) + si)
     msg = 1.0 - 2.0 * (torch.rand(int(d["n_dec"]), K) < 0.5).float()
     pac = "pac" in d.files and int(d["pac"]) == 1
-    enc = O.pac_encode if pac else O.encode_plotkin  # pac_code.py:220-224 / polar.py:128-148
-    x = torch.from_numpy(enc(msg.numpy(), N, d["info"]))
+    if pac:  # pac_code.py:220-224 with the fixture's generator (g = 91; 53 at N = 32 as rnn_all.py:231-232 sets it)
+        x = torch.from_numpy(O.pac_encode(msg.numpy(), N, d["info"], g=int(d["g"]) if "g" in d.files else 91))
+    else:  # polar.py:128-148
+        x = torch.from_numpy(O.encode_plotkin(msg.numpy(), N, d["info"]))
     sigma = 10 ** (-float(d["snr"][si]) * 1.0 / 20)
     y = x + sigma * torch.randn(x.shape, dtype=torch.float)
     yn = y.numpy()

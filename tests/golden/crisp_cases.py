@@ -50,6 +50,28 @@ CASES = {
     "trained_crisp_64_22_f512": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=22, F=512, seed_init=6422,
                                      curriculum=_cur(8, 6000, 22, 1500, 20000, 20), ref_lr=2e-4,
                                      n_logit=128, n_sc=1 << 14, n_dec=2048, n_mc=1 << 17, seed_dec=59, seed_mc=61),
+    # round 6: a scaled-down PAC decoder for configs[3]'s code family (rnn_all.py:61 --code PAC, g = 91), PAC(32,16) at
+    # configs[3]'s width (hidden 64): K = 4 .. 16 on the GPU, then the reference's own loop for a last short stage (as
+    # trained_crisp_64_22_f512).  Hard first ('rev_RM') at AdamW lr 3e-4: at the reference's 1e-3 the hard-first order
+    # (trained_pac_32_16_rev) learned through K = 10 (BLER 0.48 / 0.25 / 0.08 at 0 / 2 / 4 dB) and ended at BLER
+    # 0.93-0.98 at K = 16, and the easy-first order ('RM', trained_pac_32_16_rm) diverged at K = 11
+    # (profiles/round6/train_pac_32_16.txt; those runs used g = 91, a PAC code of pac_code.py but not the one rnn_all.py
+    # trains at N = 32, so they are GPU-only curriculum experiments)
+    # the PAC(32,16) attempts below all learned their codes through K = 10 and lost them after: the PAC fixture is the
+    # standard PAC(32,10) 'RM' code (the easy-first order's own K = 10 set), trained to its K with a long last stage.
+    # g = 53: rnn_all.py:231-232 fixes the convolution by N (53 at N = 32; 91 from N = 64), whatever --g says
+    "trained_pac_32_10": dict(_COMMON, code="PAC", profile="RM", N=32, K=10, g=53, seed_init=3210,
+                              curriculum=_cur(4, 3000, 10, 3000, 20000, 20), ref_lr=2e-4,
+                              n_logit=512, n_sc=1 << 15, seed_dec=67, seed_mc=69),
+    "trained_pac_32_16": dict(_COMMON, code="PAC", profile="rev_RM", N=32, K=16, seed_init=3219, lr=3e-4,
+                              curriculum=_cur(4, 3000, 16, 3000, 30000, 20), ref_lr=2e-4,
+                              n_logit=512, n_sc=1 << 15, seed_dec=71, seed_mc=73),
+    "trained_pac_32_16_rm": dict(_COMMON, code="PAC", profile="RM", N=32, K=16, seed_init=3218,
+                                 curriculum=_cur(4, 3000, 16, 3000, 30000, 20), ref_lr=2e-4,
+                                 n_logit=512, n_sc=1 << 15, seed_dec=71, seed_mc=73),
+    "trained_pac_32_16_rev": dict(_COMMON, code="PAC", profile="rev_RM", N=32, K=16, seed_init=3217,
+                                  curriculum=_cur(4, 3000, 16, 1500, 30000, 20), ref_lr=2e-4,
+                                  n_logit=512, n_sc=1 << 15, seed_dec=71, seed_mc=73),
     # PAC(128,64) (configs[3], rnn_all.py:61 --code PAC, rate profile 'RM' reversed = hard first) at the CRISP script's
     # own width (run_crisp.sh: --rnn_feature_size 512): K = 8 .. 64 on the GPU, then the reference's loop.  At hidden 64
     # the same curriculum stalled (per-bit BER 0.08-0.26 even at 10 dB by K = 12, in either bit order).  NOT GENERATED:

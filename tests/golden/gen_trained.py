@@ -63,6 +63,10 @@ def train(name, c, workdir, gpu_weights=None):
     continue from the GPU trainer's --out file (default train_state/<name>.net.pt)."""
     wd = os.path.join(workdir, name)
     os.makedirs(wd, exist_ok=True)
+    if c["code"] == "PAC":  # rnn_all.py:218-235 picks the convolution from N whatever --g says
+        ref_g = {4: 7, 8: 13, 16: 21, 32: 53}.get(c["N"], 91)
+        if c.get("g", 91) != ref_g:
+            raise SystemExit(f"{name}: g = {c.get('g', 91)} but rnn_all.py trains N = {c['N']} PAC codes with g = {ref_g}")
     prev = None
     seen = {}
     path = None
@@ -98,7 +102,7 @@ def train(name, c, workdir, gpu_weights=None):
                "--print_freq", "250", "--test_batch_size", "2000", "--test_size", "2000", "--model_save_per", "100000",
                "--save_path", path, "--fresh"]
         if c["code"] == "PAC":
-            cmd += ["--g", "91"]
+            cmd += ["--g", str(c.get("g", 91))]  # (rnn_all.py:218-235 sets g from N itself; crisp_cases matches it)
         if prev:
             cmd += ["--load_path", prev]
         print("train:", name, f"K={K}", f"{steps} steps", flush=True)
@@ -142,7 +146,7 @@ def evaluate(name, c, ckpt):
     if c["code"] == "Polar":
         code = rnn_m.get_code("Polar", "polar", N, K)
     else:
-        code = rnn_m.get_code("PAC", "RM", N, K, 91)
+        code = rnn_m.get_code("PAC", "RM", N, K, c.get("g", 91))
     info = np.asarray(code.info_inds, np.int64)
     with torch.serialization.safe_globals([argparse.Namespace]):
         ck = torch.load(ckpt, map_location="cpu", weights_only=True)
@@ -155,7 +159,7 @@ def evaluate(name, c, ckpt):
 
     out = {"info": info, "N": np.int64(N), "K": np.int64(K), "F": np.int64(F), "layers": np.int64(c["layers"]),
            "onehot": np.int64(1), "rev": np.int64(0), "snr": np.asarray(SNRS), "train_snr": np.float64(c["snr_train"]),
-           "pac": np.int64(c["code"] == "PAC"), "profile": np.bytes_(c["profile"]),
+           "pac": np.int64(c["code"] == "PAC"), "profile": np.bytes_(c["profile"]), "g": np.int64(c.get("g", 91)),
            # (K, steps, trainer) per stage; trainer 0 = the reference's rnn_all.py (CPU), 1 = train_crisp_gpu.py
            "curriculum": np.asarray([(k, n, int(w == "gpu")) for k, n, w in c["curriculum"]], np.int64),
            "ref_lr": np.float64(c["ref_lr"]), "train_batch": np.int64(c["batch"]),

@@ -60,8 +60,15 @@ def plotkin(u):
     return x
 
 
+def pac_taps(g):
+    """Delays j >= 1 whose generator bit is set (g_array = 1 - 2 bits(g), pac_code.py:101-103): g = 91 -> (2, 3, 5, 6),
+    g = 53 (the reference's choice at N = 32, rnn_all.py:231-232) -> (1, 3, 5)."""
+    bits = [int(ch) for ch in bin(g)[2:]]
+    return tuple(j for j in range(1, len(bits)) if bits[j] == 1)
+
+
 def pac_conv(v, taps=(2, 3, 5, 6)):
-    """PAC rate-1/1 convolution with g = 91 (pac_code.py:193-200): u_i = v_i prod_{j in taps} v_{i-j}, v_{<0} = +1."""
+    """PAC rate-1/1 convolution (pac_code.py:193-200): u_i = v_i prod_{j in taps} v_{i-j}, v_{<0} = +1 (default g = 91)."""
     B, N = v.shape
     vp = torch.cat([torch.ones(B, max(taps), device=v.device), v], 1)
     u = v.clone()
@@ -85,7 +92,7 @@ def make_code(c, K, device="cuda"):
     def enc(msg):
         u = torch.ones(msg.shape[0], N, device=msg.device)
         u[:, it] = msg
-        return plotkin(pac_conv(u) if pac else u)
+        return plotkin(pac_conv(u, pac_taps(c.get("g", 91))) if pac else u)
     return info, enc
 
 

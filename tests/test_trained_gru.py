@@ -64,11 +64,13 @@ def test_trainer_encoders_match_oracle(oracle):
     from crisp_cases import CASES
     from train_crisp_gpu import make_code
     rng = np.random.default_rng(5)
-    for name, Ks in (("trained_crisp_64_32", (8, 20, 32)), ("trained_pac_128_64_f512", (8, 37, 64))):
+    for name, Ks in (("trained_crisp_64_32", (8, 20, 32)), ("trained_pac_128_64_f512", (8, 37, 64)),
+                     ("trained_pac_32_10", (4, 7, 10))):
         c = CASES[name]
         for K in Ks:
             info, enc = make_code(c, K, torch.device("cpu"))
             msg = np.where(rng.random((300, K)) < 0.5, -1.0, 1.0).astype(np.float32)
             x = enc(torch.from_numpy(msg)).numpy()
-            ref = oracle.encode_plotkin(msg, c["N"], info) if c["code"] == "Polar" else oracle.pac_encode(msg, c["N"], info)
+            ref = (oracle.encode_plotkin(msg, c["N"], info) if c["code"] == "Polar"
+                   else oracle.pac_encode(msg, c["N"], info, g=c.get("g", 91)))
             assert np.array_equal(x, ref), (name, K)

@@ -91,7 +91,7 @@ def fixture_code(d):
     from neural_polar_decoder_amd import PAC, reference_polar_code
     N, K = int(d["N"]), int(d["K"])
     if "pac" in d.files and int(d["pac"]) == 1:
-        code = PAC(argparse.Namespace(target_K=K), N, K, 91)
+        code = PAC(argparse.Namespace(target_K=K), N, K, int(d["g"]) if "g" in d.files else 91)
         info = np.asarray(code.B)
     else:
         code = reference_polar_code(N, K)

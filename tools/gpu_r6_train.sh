@@ -1,10 +1,10 @@
 #!/bin/bash
-# round 6: one slice of the full run_crisp.sh schedule for configs[2]'s decoder (Polar(64,32) rev_polar, hidden 64;
-# tests/golden/crisp_cases.py trained_crisp_64_32_full), HIP-graph replayed training steps.  The resumable state travels
+# round 6: one slice of a GPU curriculum from tests/golden/crisp_cases.py (CASE, default configs[2]'s decoder on the full
+# run_crisp.sh schedule, trained_crisp_64_32_full), HIP-graph replayed training steps.  The resumable state travels
 # in train_r6/ (uploaded with the tree; copy gpurun_out/train/$C.pt there after each call).
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/train
-C=trained_crisp_64_32_full
+C=${CASE:-trained_crisp_64_32_full}
 [ -f train_r6/$C.pt ] && cp train_r6/$C.pt gpurun_out/train/$C.pt
 timeout -k 10 $((${BUDGET:-960} + 150)) python -u tests/golden/train_crisp_gpu.py $C --state gpurun_out/train/$C.pt \
     --out gpurun_out/train/$C.net.pt --budget-s ${BUDGET:-960} --graph --eval-every 5000 > gpurun_out/train/$C.txt 2>&1
