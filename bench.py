@@ -439,20 +439,33 @@ def db_bar(snrs, bler, n, ref_bler, nr):
     return {"points": pts, "resolvable_points": n_res, "ber_match_0.05dB": bool(ok and n_res >= 2)}
 
 
-def decoding_net_leg(dev, rank, world, timer, B=1 << 20):
+TRAINED_PAC_32_10 = os.path.join(ROOT, "tests", "golden", "trained_pac_32_10.npz")
+
+
+def decoding_net_leg(dev, rank, world, timer, B=1 << 20, path=TRAINED_32_16):
     """The headline's GRU kernel (gru16p_kernel<5>, fp16x3, the same fused sweep + count launch) on a net that DECODES:
     tests/golden/trained_crisp_32_16.npz (Polar(32,16) rev_polar CRISP GRU hidden 64, 2 layers; reference BLER 0.73 ->
     0.16 over 0-4 dB, its final stage trained by the reference's rnn_all.py).  2^20 Philox words per SNR per GPU, BER /
     BLER against the reference's own Monte-Carlo curve for the same weights (2^20 words per SNR through
     RNN_decoder.decode on the CPU): z-tests and the +-0.05 dB bar.  The headline net (Polar(64,32) hidden 64) does not
-    decode (BLER ~ 1), so this record is where the headline kernel's BER match is measured."""
-    if not os.path.exists(TRAINED_32_16):
+    decode (BLER ~ 1), so this record is where the headline kernel's BER match is measured.  With
+    path = tests/golden/trained_pac_32_10.npz the same record for configs[3]'s code family: a PAC(32,10) CRISP GRU
+    (g = 53, hidden 64; reference BLER 0.22 -> 0.017 over 0-4 dB) on the same kernel, counted against the PAC message."""
+    if not os.path.exists(path):
         return None
-    from neural_polar_decoder_amd import reference_polar_code
-    code = reference_polar_code(32, 16)
-    net, dec, wdesc, fix = trained_or_seeded(code, TRAINED_32_16, code.info_positions, dev, precision="fp16x3")
+    import argparse as _ap
+    from neural_polar_decoder_amd import PAC, reference_polar_code
+    d = np.load(path)
+    N, K = int(d["N"]), int(d["K"])
+    if "pac" in d.files and int(d["pac"]) == 1:
+        code = PAC(_ap.Namespace(target_K=K), N, K, int(d["g"]) if "g" in d.files else 91)
+        info = code.B
+    else:
+        code = reference_polar_code(N, K)
+        info = code.info_positions
+    net, dec, wdesc, fix = trained_or_seeded(code, path, info, dev, precision="fp16x3")
     snrs = [float(x) for x in fix["snr"]]
-    yall = torch.empty(len(snrs), B, 32, dtype=torch.float32, device=dev)
+    yall = torch.empty(len(snrs), B, N, dtype=torch.float32, device=dev)
     msg = None
     for si, s_ in enumerate(snrs):
         m, _, _ = code.mc_generate(B, s_, SEED + 1, si, rank * B, want_msg=msg is None, out=yall[si])
@@ -470,12 +483,13 @@ def decoding_net_leg(dev, rank, world, timer, B=1 << 20):
     return {"value": world * len(snrs) * B / t, "unit": "codewords/s", "ms_per_sweep": t * 1e3,
             "kernel": "gru16p_kernel<5> (fp16x3, npd_gru_decode_count_sweep: 5 SNR points in one launch)",
             "weights": wdesc, "words_per_snr": n,
-            "ber": {str(s_): float(cc[i, 0]) / (n * 16) for i, s_ in enumerate(snrs)},
+            "ber": {str(s_): float(cc[i, 0]) / (n * K) for i, s_ in enumerate(snrs)},
             "bler": {str(s_): b for s_, b in zip(snrs, bler)},
             "bler_reference": {str(s_): b for s_, b in zip(snrs, ref_bler)},
-            "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, 16),
+            "gru_vs_reference": gru_vs_reference(fix, snrs, cc[:, 0], cc[:, 1], n, K),
             "db_bar": db_bar(snrs, bler, n, ref_bler, nr),
-            "config": "Polar(32,16) CRISP GRU hidden 64, 2 layers (trained, decodes), 0-4 dB, 2^20 words per SNR per GPU"}
+            "config": f"{'PAC' if isinstance(code, PAC) else 'Polar'}({N},{K}) CRISP GRU hidden 64, 2 layers (trained, "
+                      f"decodes), 0-4 dB, 2^20 words per SNR per GPU"}
 
 
 TRAINED_F512 = os.path.join(ROOT, "tests", "golden", "trained_crisp_64_22_f512.npz")
@@ -1048,6 +1062,8 @@ def main():
         legs["crisp_gru_f512"] = crisp_f512_leg(dev, rank, world, timer)
     if not (args.no_gru and args.no_pac):
         legs.update(pac_legs(snrs, B, rank, world, timer, dev, not args.no_gru, not args.no_pac))
+    if not args.no_gru:
+        legs["pac_gru_decoding_net"] = decoding_net_leg(dev, rank, world, timer, path=TRAINED_PAC_32_10)
     if not args.no_scl:
         legs["scl"] = scl_leg(code, dev, ys[2], snrs[2], world, timer)
     if not args.no_lse:
@@ -1126,6 +1142,11 @@ def compact_configs(legs, gvr):
     if "pac_gru" in legs:
         c["3_pac_gru"] = {"value": r3(legs["pac_gru"]["value"]), "fp16_issued_frac": r3(legs["pac_gru"]["issued_frac"]),
                           "fp32_path": r3(legs["pac_gru"]["fp32_path"]["value"])}
+    pn = legs.get("pac_gru_decoding_net")
+    if pn is not None and "3_pac_gru" in c:
+        # configs[3]'s kernel on a PAC net that decodes (scaled down: PAC(32,10), g = 53, hidden 64)
+        c["3_pac_gru"]["trained_scaled_down_ber_match_0.05dB"] = pn["db_bar"]["ber_match_0.05dB"]
+        c["3_pac_gru"]["trained_scaled_down_within_4_sigma"] = pn["gru_vs_reference"]["within_4_sigma"]
     if "pac_sc" in legs:
         c["3_pac_sc"] = {"value": r3(legs["pac_sc"]["value"]), "hbm_frac": r3(legs["pac_sc"]["roofline"]["frac"])}
     if "conv_model" in legs:

@@ -15,7 +15,8 @@ from conftest import trained_decisions, trained_fixture, trained_words
 LOGIT_ATOL = 1e-4
 
 
-@pytest.mark.parametrize("name", ["trained_crisp_32_16", "trained_crisp_64_32", "trained_crisp_64_22_f512"])
+@pytest.mark.parametrize("name", ["trained_crisp_32_16", "trained_crisp_64_32", "trained_crisp_64_22_f512",
+                                  "trained_pac_32_10"])
 def test_oracle_gru_trained_fixture(oracle, name):
     d = trained_fixture(name)
     N, F, L = int(d["N"]), int(d["F"]), int(d["layers"])

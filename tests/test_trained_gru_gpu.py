@@ -29,11 +29,12 @@ DEV = "cuda:0"
 # trained recurrences amplify rounding: the reference's own fp32 logits sit up to 2.2e-5 (Polar(64,32)) / 7.3e-6
 # (Polar(32,16)) from float64 on the fixture words, so two fp32-class implementations are held to 1e-4 of each other
 LOGIT_ATOL = 1e-4
-CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_crisp_64_22_f512"]
+CASES = ["trained_crisp_32_16", "trained_crisp_64_32", "trained_crisp_64_22_f512", "trained_pac_32_10"]
 # fixtures whose reference BLER curve falls inside the dB bar's domain ([1e-3, 0.9]) at two or more SNR points; the
 # hidden-64 Polar(64,32) net never learned to decode (BLER ~ 1 over 0-4 dB): z-tests only.  The
-# hidden-512 Polar(64,22) net is run_crisp.sh's own decoder (rev_polar curriculum, gru_wide_kernel).
-DB_CASES = {"trained_crisp_32_16", "trained_crisp_64_22_f512"}
+# hidden-512 Polar(64,22) net is run_crisp.sh's own decoder (rev_polar curriculum, gru_wide_kernel); the PAC(32,10) net
+# (g = 53, as rnn_all.py trains N = 32 PAC codes) is configs[3]'s code family at configs[3]'s width, scaled down.
+DB_CASES = {"trained_crisp_32_16", "trained_crisp_64_22_f512", "trained_pac_32_10"}
 
 
 def build(d, precision="fp32"):
