@@ -106,3 +106,9 @@ def pac_info_positions(N: int, K: int, scheme: str = "RM", target_K: int | None 
     else:
         raise ValueError(f"unsupported PAC rate profile {scheme!r} (polar/custom need data files absent from the reference)")
     return np.sort(np.asarray(B)).astype(np.int64)
+
+
+def pac_default_g(N: int) -> int:
+    """The PAC convolution polynomial the reference's scripts use for length N: rnn_all.py:218-235, run_models.py:197-213
+    and rnn.py:224-240 overwrite --g from N (7, 13, 21, 53 at N = 4, 8, 16, 32; 91 otherwise)."""
+    return {4: 7, 8: 13, 16: 21, 32: 53}.get(int(N), 91)

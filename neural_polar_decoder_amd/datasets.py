@@ -18,7 +18,7 @@ import os
 import numpy as np
 import torch
 
-from .codes import pac_info_positions, polar_info_positions
+from .codes import pac_default_g, pac_info_positions, polar_info_positions
 
 
 # ------------------------------------------------------------------------------------ test sets
@@ -115,7 +115,7 @@ def code_from_args(args):
     tK = getattr(args, "target_K", None)
     rp = getattr(args, "rate_profile", "polar")
     if kind == "pac":
-        return PAC(argparse.Namespace(target_K=tK or K), N, K, int(getattr(args, "g", 91)), rate_profile=rp)
+        return PAC(argparse.Namespace(target_K=tK or K), N, K, int(getattr(args, "g", pac_default_g(N))), rate_profile=rp)
     info = polar_info_positions(N, K, rp, tK)
     return PolarCode(int(np.log2(N)), K, F=np.setdiff1d(np.arange(N), info))
 

@@ -263,7 +263,8 @@ def _main(argv=None):
     ap.add_argument("--K", type=int, default=32)
     ap.add_argument("--rate_profile", default="polar")
     ap.add_argument("--target_K", type=int, default=None)
-    ap.add_argument("--g", type=int, default=91)
+    ap.add_argument("--g", type=int, default=None, help="PAC polynomial (default: the reference scripts' choice for N, "
+                                                         "codes.pac_default_g: 53 at N = 32, 91 from N = 64)")
     ap.add_argument("--test_snr_start", type=float, default=0.0)
     ap.add_argument("--test_snr_end", type=float, default=4.0)
     ap.add_argument("--snr_points", type=int, default=5)
@@ -288,8 +289,10 @@ def _main(argv=None):
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from .codes import polar_info_positions
+    from .codes import pac_default_g, polar_info_positions
     from .pac_code import PAC
+    if a.g is None:
+        a.g = pac_default_g(a.N)
     from .polar import PolarCode
     if a.code == "polar":
         info = polar_info_positions(a.N, a.K, a.rate_profile, a.target_K)

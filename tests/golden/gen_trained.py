@@ -47,6 +47,7 @@ import torch  # noqa: E402
 SNRS = [0.0, 1.0, 2.0, 3.0, 4.0]
 
 sys.path.insert(0, OUT)
+sys.path.insert(1, os.path.dirname(os.path.dirname(OUT)))  # the repository root (neural_polar_decoder_amd)
 from crisp_cases import CASES  # noqa: E402
 
 TRAIN_STATE = os.path.join(os.path.dirname(os.path.dirname(OUT)), "train_state")
@@ -64,7 +65,8 @@ def train(name, c, workdir, gpu_weights=None):
     wd = os.path.join(workdir, name)
     os.makedirs(wd, exist_ok=True)
     if c["code"] == "PAC":  # rnn_all.py:218-235 picks the convolution from N whatever --g says
-        ref_g = {4: 7, 8: 13, 16: 21, 32: 53}.get(c["N"], 91)
+        from neural_polar_decoder_amd.codes import pac_default_g
+        ref_g = pac_default_g(c["N"])
         if c.get("g", 91) != ref_g:
             raise SystemExit(f"{name}: g = {c.get('g', 91)} but rnn_all.py trains N = {c['N']} PAC codes with g = {ref_g}")
     prev = None

@@ -251,3 +251,10 @@ def test_sc_decode_soft_new_golden(oracle, N, K):
             assert np.all(err <= 2 * el[ok]), (N, ptag, float((err / np.maximum(2 * el[ok], 1e-300)).max()))
             bad = oracle.unexplained_disagreements(hat, d[f"msg_hat_{ptag}"][m], d["info"], lf, el, False)
             assert not bad, (N, ptag, bad[:3])
+
+
+def test_pac_default_polynomial_follows_the_reference_scripts():
+    """rnn_all.py:218-235 / run_models.py:197-213 / rnn.py:224-240 overwrite --g from N; the MC CLI and the checkpoint
+    loader default to the same choice, so a PAC(32, K) net the reference trained (g = 53) meets its own code."""
+    from neural_polar_decoder_amd.codes import pac_default_g
+    assert [pac_default_g(N) for N in (4, 8, 16, 32, 64, 128, 256)] == [7, 13, 21, 53, 91, 91, 91]
