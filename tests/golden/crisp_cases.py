@@ -43,6 +43,12 @@ CASES = {
     "trained_crisp_64_32_full": dict(_COMMON, code="Polar", profile="rev_polar", N=64, K=32, seed_init=6434,
                                      curriculum=_cur(8, 10000, 32, 5000, 100000, 1000), ref_lr=2e-4,
                                      n_logit=256, n_sc=1 << 16, seed_dec=41, seed_mc=43),
+    # round 6: run_crisp.sh's code at configs[2]'s width -- Polar(64,22) hidden 64 -- on the easy-first order ('polar')
+    # with a long last stage, for a decoding net on the headline kernel's own length (N = 64).  NOT GENERATED: learned
+    # through K = 16 and diverged in the K = 17 stage (profiles/round6/train_crisp_64_22_h64.txt)
+    "trained_crisp_64_22": dict(_COMMON, code="Polar", profile="polar", N=64, K=22, seed_init=6423,
+                                curriculum=_cur(8, 3000, 22, 2000, 20000, 20), ref_lr=2e-4,
+                                n_logit=256, n_sc=1 << 16, seed_dec=79, seed_mc=83),
     # run_crisp.sh's own decoder: Polar(64,22), rate profile rev_polar (hard first), GRU hidden 512, 2 layers, onehot
     # y_input, K = 8 .. 22 with K + 1 per stage.  The script runs 10000 steps at K = 8, 5000 per later stage and 100000 at
     # K = 22 (175k steps); this case runs the same stage order on the GPU with shortened stages (a GPU-minute budget),
